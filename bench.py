@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident pack + unpack of Quad{4 x int32} records.
+
+BASELINE.json metric: "packer GiB/s + Mrecords/s device-resident, 1/2/4/8 MI355X".
+One step = one pass of the hot path over one batch of synthetic records
+already resident in HBM: srpc_gpu_pack (4 int32 columns -> 16-byte wire
+records) followed by srpc_gpu_unpack (wire -> 4 columns), both through the
+C ABI of srpc_amd/libsrpc_gpu.so.  Weak scaling: every rank owns 16M records
+(configs[2] of BASELINE.json per GPU; at 4 GPUs that is configs[3]'s 64M).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  `value` = wire GiB/s through a full
+pack+unpack round trip summed over all ranks (records * 16 B / 2^30 / step
+time, the max over ranks).  The roofline object prices the dominant kernel
+against HBM3E (8.0 TB/s spec) with algorithmic bytes (32 B per record per
+kernel); the cpu_baseline object times the reference packer (compiled from
+/root/reference into oracle/_ref, or the C restatement if that is absent) on
+this host.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+HBM_MEASURED_COPY_GBPS = 6290.0  # measured float4 copy ceiling (same table)
+REC_BYTES = 16                  # Quad body
+ALG_BYTES_PER_REC = 32          # per kernel: pack reads 4x4 B + writes 16 B; unpack the reverse
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--records", type=int, default=1 << 24, help="records per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU-baseline work (rank 0, N=1 only); 0 disables")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--path", choices=["auto", "dword", "tile"], default="auto")
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, target_s: float) -> dict | None:
+    """The reference CPU packer on this host: pack (`p << r` per record) +
+    unpack (`r.unpack(bp)` per record) of the same Quad workload, repeated
+    until ~target_s seconds of CPU work.  Rank 0, N=1 only."""
+    import ctypes as C
+
+    import numpy as np
+
+    import oracle
+
+    m = min(n, 1 << 22)  # 4M-record slices of the same splitmix stream
+    cols = oracle.splitmix_columns_i32(4, m)
+    wire = np.zeros(m * 16, np.uint8)
+    back = [np.zeros(m, np.int32) for _ in range(4)]
+    if oracle.ref_available():
+        ref = oracle.ref_lib()
+        kind = "reference"
+        tp, tu = C.c_double(0), C.c_double(0)
+
+        def one():
+            ref.ref_pack_quad(*[c.ctypes.data for c in cols], m, wire.ctypes.data, wire.size,
+                              C.byref(tp))
+            ref.ref_unpack_quad(wire.ctypes.data, wire.size, m, *[b.ctypes.data for b in back],
+                                C.byref(tu))
+            return tp.value + tu.value
+    else:
+        kind = "port"
+
+        def one():
+            t0 = time.perf_counter()
+            w = oracle.pack([oracle.INT32] * 4, cols, m)
+            oracle.unpack([oracle.INT32] * 4, w, m)
+            return time.perf_counter() - t0
+    total, recs = 0.0, 0
+    while True:
+        total += one()
+        recs += m
+        if total >= target_s or recs >= 64 * m:
+            break
+    gib = recs * REC_BYTES / 2**30
+    out = {"value": round(gib / total, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+           "sample": f"{recs} Quad records ({recs // m} passes over a {m}-record slice of the "
+                     f"same splitmix stream), pack+unpack, 1 thread, {total:.1f} s",
+           "mrecords_per_s": round(recs / total / 1e6, 2)}
+    if kind == "reference":
+        nt = max(1, min(os.cpu_count() or 1, 16))
+        ts = C.c_double(0)
+        tu = C.c_double(0)
+        ref.ref_pack_quad_mt(*[c.ctypes.data for c in cols], m, wire.ctypes.data, nt, C.byref(ts))
+        ref.ref_unpack_quad_mt(wire.ctypes.data, m, *[b.ctypes.data for b in back], nt, C.byref(tu))
+        out["multithread"] = {"threads": nt, "value": round(m * REC_BYTES / 2**30 / (ts.value + tu.value), 4),
+                              "sample": f"{m} records, one packer per contiguous shard"}
+    return out
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import srpc_amd
+    from srpc_amd import QUAD, GpuPacker, _lib
+    from srpc_amd.shard import gather_packed
+
+    n = args.records
+    first = rank * n  # the global batch is one splitmix stream sharded contiguously
+    p = GpuPacker(QUAD, device=local)
+    if args.path != "auto":
+        p.force_path({"dword": srpc_amd.SRPC_PATH_DWORD, "tile": srpc_amd.SRPC_PATH_TILE}[args.path])
+    stream = torch.cuda.current_stream(dev)
+    cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
+    back = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
+    wire = torch.empty(n * REC_BYTES, dtype=torch.uint8, device=dev)
+    srpc_amd.fill_splitmix_i32(cols, n, 0x5EED, first, stream)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        p.pack(cols, n, wire, stream=stream)
+        p.unpack(wire, n * REC_BYTES, n, back, stream=stream)
+
+    # correctness of the exact bytes being timed: round trip + reference digest
+    verify = {}
+    if not args.no_verify:
+        step()
+        torch.cuda.synchronize(dev)
+        ok = all(torch.equal(a, b) for a, b in zip(cols, back))
+        verify["roundtrip"] = bool(ok)
+        full = gather_packed(wire, REC_BYTES, n * world) if world > 1 else wire
+        if rank == 0:
+            digest = hashlib.sha256(full.cpu().numpy().tobytes()).hexdigest()
+            with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
+                streams = json.load(f)["streams"]
+            want = {1 << 24: streams["quad_body_16M"]["sha256"],
+                    1 << 26: streams["quad_body_64M"]["sha256"]}.get(n * world)
+            verify["sha256"] = digest
+            verify["matches_reference"] = (digest == want) if want else None
+        if world > 1:
+            flag = torch.tensor([int(ok)], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            verify["roundtrip"] = bool(flag.item())
+        del full
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    K = args.steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        p.pack(cols, n, wire, stream=stream)
+        ev[i][1].record(stream)
+        p.unpack(wire, n * REC_BYTES, n, back, stream=stream)
+        ev[i][2].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    pack_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(K)]
+    unpack_ms = [ev[i][1].elapsed_time(ev[i][2]) for i in range(K)]
+    gpu_ms = ev[0][0].elapsed_time(ev[K - 1][2])
+    t_rank = max(elapsed, gpu_ms / 1e3)
+    t = torch.tensor([t_rank, sum(pack_ms) / K, sum(unpack_ms) / K], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max, pack_avg, unpack_avg = t.tolist()
+    ms_step = t_max * 1e3 / K
+
+    # gather of the packed shards to rank 0 over RCCL (reported separately)
+    gather = None
+    if world > 1:
+        for _ in range(2):
+            gather_packed(wire, REC_BYTES, n * world)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            gather_packed(wire, REC_BYTES, n * world)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g_ms = (time.perf_counter() - g0) * 1e3 / reps
+        moved = n * (world - 1) * REC_BYTES
+        gather = {"ms": round(g_ms, 3), "bytes_to_root": moved,
+                  "root_ingress_GBps": round(moved / g_ms / 1e6, 1),
+                  "collective": "RCCL gather (ncclSend/ncclRecv to rank 0)"}
+
+    # PCIe-inclusive round trip (host columns -> device -> wire -> host), rank 0 only
+    pcie = None
+    if rank == 0 and world == 1 and not args.no_pcie:
+        hcols = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(4)]
+        hwire = torch.empty(n * REC_BYTES, dtype=torch.uint8).pin_memory()
+        for h, c in zip(hcols, cols):
+            h.copy_(c)
+        torch.cuda.synchronize(dev)
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        reps = 3
+        s0.record(stream)
+        for _ in range(reps):
+            for h, c in zip(hcols, cols):
+                c.copy_(h, non_blocking=True)
+            p.pack(cols, n, wire, stream=stream)
+            hwire.copy_(wire, non_blocking=True)
+        s1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = s0.elapsed_time(s1) / reps
+        pcie = {"what": "H2D columns + pack + D2H wire (pinned, one stream)",
+                "ms": round(ms, 3), "wire_GiBps": round(n * REC_BYTES / 2**30 / (ms / 1e3), 3),
+                "mrecords_per_s": round(n / (ms / 1e3) / 1e6, 1)}
+
+    if rank == 0:
+        total_recs = n * world
+        value = total_recs * REC_BYTES / 2**30 / (t_max)  * K
+        dom_name, dom_ms = ("pack", pack_avg) if pack_avg >= unpack_avg else ("unpack", unpack_avg)
+        achieved = ALG_BYTES_PER_REC * n / (dom_ms / 1e3) / 1e9
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(prof):
+            with open(prof) as f:
+                pm = json.load(f)
+            ent = pm.get("kernels", {}).get(dom_name)
+            if ent and pm.get("records") == n:
+                traffic = ent.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "packer GiB/s + Mrecords/s device-resident, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (splitmix64 stream of SURVEY.md §8c, generated in HBM)",
+            "config": {"workload": "Quad{4 x int32} pack+unpack, 16-byte records, device-resident",
+                       "records_per_gpu": n, "global_records": total_recs,
+                       "record_bytes": REC_BYTES, "parallelism": f"shard{world}",
+                       "kernel_path": {1: "dword", 2: "tile"}[p.path]},
+            "mrecords_per_s": round(total_recs * K / t_max / 1e6, 1),
+            "hbm_algorithmic_GBps": round(2 * ALG_BYTES_PER_REC * total_recs * K / t_max / 1e9, 1),
+            "kernels_ms": {"pack": round(pack_avg, 4), "unpack": round(unpack_avg, 4)},
+            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "frac_of_measured_copy": round(achieved / HBM_MEASURED_COPY_GBPS, 4),
+                         "alg_bytes_per_launch": ALG_BYTES_PER_REC * n,
+                         "traffic": traffic},
+            "verify": verify,
+        }
+        if gather:
+            line["gather"] = gather
+        if pcie:
+            line["pcie_inclusive"] = pcie
+        if world == 1 and args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        line["native_lib"] = _lib.so_path()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * srpc_gpu.h -- C ABI of the MI355X (gfx950) batched sRPC packer.
+ *
+ * This is the drop-in boundary for the reference's packer hot path.  The
+ * reference has no FFI of its own: its "operator API" is the header-only C++
+ * template surface of namespace srpc (include/srpc/packer.hpp:53-181).  Each
+ * entry point below replaces a loop over one of those calls with one batched,
+ * stream-ordered launch over N records:
+ *
+ *   srpc_gpu_pack    <- `packer p; for (r : batch) p << r;`
+ *                       (packer.hpp:73 -> pack_arg 183-191 -> pack_struct 172-178),
+ *                       and, with a request/response prefix, the loops over
+ *                       pack_request (packer.hpp:77-82) / pack_response (86-91)
+ *   srpc_gpu_unpack  <- `for (r : batch) r.unpack(bp);` (generated unpack,
+ *                       examples/calculator_srpc.cpp:19-22, calling
+ *                       packer::operator>> 70 -> pipe_output 210-222), and,
+ *                       with a prefix, unpack_request / unpack_response / getv
+ *                       (packer.hpp:95-162) for records of one known type
+ *   srpc_plan_create <- the compile-time reflection over T::fields
+ *                       (core.hpp:9-14, STRUCT_MEMBER) that fixes field order
+ *                       and sizes; the C++ side (include/srpc/gpu.hpp) builds
+ *                       the descriptor from T::fields automatically.
+ *
+ * Wire bytes are identical to the reference's: raw little-endian fields in
+ * declaration order, no padding, nested messages inlined, strings as a u64
+ * length followed by the bytes, records back to back.
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers (hipMalloc'd) unless named h_*.
+ *     The library allocates nothing on the pack/unpack hot path.
+ *   - `stream` is a hipStream_t (NULL = the default stream).  Calls are
+ *     asynchronous and stream-ordered; they are safe to capture in a hipGraph.
+ *   - Return values: 0 = launched; <0 = argument / HIP error (nothing launched);
+ *     >0 = a data error detected on the host (see SRPC_ERR_*).  No exception
+ *     ever crosses this ABI (the reference terminates instead: core.hpp:28-33
+ *     throws inside noexcept functions).
+ *   - Threading: a plan is immutable after creation and may be used from any
+ *     host thread and on any stream of its device concurrently.
+ */
+#ifndef SRPC_GPU_H
+#define SRPC_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRPC_GPU_ABI_VERSION 1
+
+/* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
+ * Nested message fields are flattened into their members by the caller. */
+typedef enum srpc_kind {
+    SRPC_KIND_BOOL = 1,   /* bool    : 1 byte               */
+    SRPC_KIND_INT8 = 2,   /* int8_t  : 1 byte               */
+    SRPC_KIND_CHAR = 3,   /* char    : 1 byte               */
+    SRPC_KIND_INT16 = 4,  /* int16_t : 2 bytes LE           */
+    SRPC_KIND_INT32 = 5,  /* int32_t : 4 bytes LE           */
+    SRPC_KIND_INT64 = 6,  /* int64_t : 8 bytes LE           */
+    SRPC_KIND_STRING = 7  /* u64 LE length + raw bytes      */
+} srpc_kind;
+
+/* Return codes. */
+#define SRPC_OK 0
+#define SRPC_E_INVALID (-1)     /* bad argument or schema                       */
+#define SRPC_E_ALIGN (-2)       /* a device pointer violates the alignment rule */
+#define SRPC_E_HIP (-3)         /* HIP runtime / launch failure                 */
+#define SRPC_E_UNSUPPORTED (-4) /* schema shape this build has no kernel for    */
+#define SRPC_E_CAPACITY (-5)    /* output buffer too small                      */
+#define SRPC_ERR_BOUNDS 2       /* wire shorter than n records; the records that
+                                   fit were decoded, the status says where the
+                                   first missing one starts                      */
+
+/* Device-side decode status bits (srpc_unpack_status.flags). */
+#define SRPC_STATUS_PREFIX 1u   /* a record's envelope header != the plan's prefix */
+#define SRPC_STATUS_BOUNDS 2u   /* a record (or string) ran past the wire end      */
+
+/* Written by srpc_gpu_unpack when its d_status argument is non-NULL.
+ * Reset by the call itself (stream-ordered) before decoding starts. */
+typedef struct srpc_unpack_status {
+    uint32_t flags;             /* OR of SRPC_STATUS_* over the batch          */
+    uint32_t reserved;
+    uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */
+} srpc_unpack_status;
+
+/* A flat record schema: fields in T::fields declaration order
+ * (packer.hpp:172-178), plus an optional constant per-record header: the
+ * `u64 len | method | u64 len | T::name` of pack_request, or the
+ * `u8 code | u64 len | T::name` of pack_response. */
+typedef struct srpc_schema_desc {
+    uint32_t nfields;
+    const int32_t* kinds;   /* host array of nfields srpc_kind values */
+    const uint8_t* prefix;  /* host bytes, may be NULL when prefix_len == 0 */
+    uint32_t prefix_len;
+} srpc_schema_desc;
+
+typedef struct srpc_plan srpc_plan;
+
+/* Which kernel family a plan runs (srpc_plan_info). */
+#define SRPC_PATH_DWORD 1   /* every field 4/8 B, no prefix, record <= 32 B:
+                               one record per lane, register-assembled records          */
+#define SRPC_PATH_TILE 2    /* any fixed-size schema: LDS-staged tiles, 16 B global I/O  */
+#define SRPC_PATH_VAR 3     /* string fields: per-record sizes + wavefront/device scan   */
+
+/* Validate a schema and prepare its kernels on `device` (allocates the
+ * plan's small device-side prefix copy; never called on the hot path). */
+int srpc_plan_create(const srpc_schema_desc* desc, int device, srpc_plan** out);
+int srpc_plan_destroy(srpc_plan* plan);
+
+/* Fixed wire bytes per record (prefix included); 0 for string schemas. */
+int srpc_plan_record_bytes(const srpc_plan* plan, uint64_t* out);
+/* Kernel family in use (SRPC_PATH_*). */
+int srpc_plan_path(const srpc_plan* plan, int* out);
+/* Testing hook: force a kernel family the schema is eligible for
+ * (SRPC_PATH_TILE is valid for every fixed schema). */
+int srpc_plan_force_path(srpc_plan* plan, int path);
+
+/* Pack n records.  d_cols[f] (host array of nfields device pointers) holds
+ * n elements of field f's C type, 4-byte aligned (16-byte for the TILE
+ * path).  d_wire receives n * record_bytes bytes; wire_cap is its size.
+ * d_wire must be 16-byte aligned. */
+int srpc_gpu_pack(const srpc_plan* plan, const void* const* d_cols, uint64_t n,
+                  uint8_t* d_wire, uint64_t wire_cap, void* stream);
+
+/* Unpack n records from wire_len bytes at d_wire into the columns d_cols.
+ * Every record's prefix is checked against the plan's; mismatches are
+ * reported in *d_status (if non-NULL), and the record's fields are still
+ * decoded from their fixed positions.  If wire_len < n * record_bytes the
+ * records that fit are decoded and SRPC_ERR_BOUNDS is returned (status
+ * flags BOUNDS, first_bad_record = wire_len / record_bytes). */
+int srpc_gpu_unpack(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len,
+                    uint64_t n, void* const* d_cols, srpc_unpack_status* d_status,
+                    void* stream);
+
+/* ---- variable-length (string) schemas -------------------------------------
+ * String field f is given as chars d_cols[f] plus n+1 u64 byte offsets
+ * d_str_offs[f] (offsets[0] may be nonzero; lengths are offs[i+1]-offs[i]).
+ * Pack writes the record start offsets (n+1 values, [0] = 0, [n] = total
+ * bytes) to d_rec_offs and needs `scratch_bytes` of device scratch from
+ * srpc_plan_var_scratch_bytes. */
+int srpc_plan_var_scratch_bytes(const srpc_plan* plan, uint64_t n, uint64_t* out);
+int srpc_gpu_pack_var(const srpc_plan* plan, const void* const* d_cols,
+                      const uint64_t* const* d_str_offs, uint64_t n, uint8_t* d_wire,
+                      uint64_t wire_cap, uint64_t* d_rec_offs, void* d_scratch,
+                      uint64_t scratch_bytes, void* stream);
+
+/* ---- utilities --------------------------------------------------------------*/
+
+/* Synthetic input of SURVEY.md §8c: nfields int32 columns, record i field f =
+ * low 32 bits of splitmix64 draw number (first_record + i) * nfields + f + 1
+ * from state `seed`.  Used by bench.py to build inputs in HBM. */
+int srpc_gpu_fill_splitmix_i32(int32_t* const* d_cols, uint32_t nfields, uint64_t n,
+                               uint64_t seed, uint64_t first_record, void* stream);
+
+const char* srpc_status_string(int code);
+int srpc_gpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRPC_GPU_H */

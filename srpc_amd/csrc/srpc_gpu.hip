@@ -1,0 +1,719 @@
+// srpc_gpu.hip -- MI355X (gfx950) batched record packer for sRPC wire format.
+//
+// Implements include/srpc_gpu.h.  Two kernel families for fixed-size schemas:
+//
+//  DWORD path  (every field 4 or 8 bytes, no envelope prefix, record <= 32 B)
+//      One record per lane.  Each record dword is read straight from its field
+//      column (lanes of a wave read consecutive elements: 256 B coalesced per
+//      wave instruction), assembled in VGPRs and stored as the widest aligned
+//      vector (dwordx4 for 16-byte records: a wave writes 1 KiB contiguous).
+//      Unpack is the transpose back.  Pure HBM streaming; no LDS, no MFMA.
+//
+//  TILE path   (any fixed-size schema: 1/2/8-byte fields, odd record strides
+//               such as the 53-byte Calculator.square request)
+//      A workgroup owns a tile of R records (R*stride bytes, a multiple of 16).
+//      Pack: 16-byte column loads -> scatter of each element into an LDS image
+//      of the tile's wire bytes -> 16-byte aligned stores of the image, with
+//      the constant envelope prefix merged from a periodic template.  Unpack:
+//      16-byte wire loads (prefix checked against the template/mask) -> LDS
+//      image -> gather of each column's elements -> 16-byte column stores.
+//
+// Wire format (reference include/srpc/packer.hpp): fields are raw LE bytes in
+// declaration order with no padding (pack_arg 183-191, pack_struct 172-178);
+// request/response envelopes are a constant header for a batch of one message
+// type and one method (pack_request 77-82, pack_response 86-91).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+
+#include "srpc_gpu.h"
+
+namespace {
+
+constexpr int kBlock = 256;          // 4 waves of 64
+constexpr int kMaxFields = 32;
+constexpr int kMaxDwords = 8;        // DWORD path: records of up to 32 bytes
+constexpr uint32_t kTileTarget = 8192;   // TILE path: ~8 KiB LDS image per tile
+constexpr uint32_t kMaxTileStride = 2048;
+constexpr uint32_t kMaxPrefix = 1024;
+
+// ---------------------------------------------------------------------------
+// Kernel argument blocks (all wave-uniform: they live in SGPRs / kernarg).
+// ---------------------------------------------------------------------------
+struct DwordMap {
+    // Record dword k = dword (r << lg[k]) of src[k]: src[k] already points at
+    // the right half of an 8-byte field, lg[k] is 0 for 4-byte fields and 1
+    // for 8-byte ones.
+    const uint32_t* src[kMaxDwords];
+    uint32_t lg[kMaxDwords];
+};
+
+struct TileArgs {
+    const uint8_t* col[kMaxFields];  // field column base (pack: src, unpack: dst)
+    uint32_t size[kMaxFields];       // field bytes: 1, 2, 4 or 8
+    uint32_t lgsize[kMaxFields];     // log2(size)
+    uint32_t off[kMaxFields];        // field byte offset inside the record (prefix included)
+    const uint8_t* prefix;           // device copy of the constant header
+    uint32_t nfields;
+    uint32_t stride;                 // record bytes
+    uint32_t prefix_len;
+    uint32_t R;                      // records per tile (multiple of 16)
+    uint32_t L;                      // template period lcm(stride, 16), divides R*stride
+};
+
+__device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag, uint64_t rec) {
+    atomicOr(&st->flags, flag);
+    atomicMin(reinterpret_cast<unsigned long long*>(&st->first_bad_record),
+              static_cast<unsigned long long>(rec));
+}
+
+// ---------------------------------------------------------------------------
+// DWORD path
+// ---------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void store_record(uint8_t* p, const uint32_t (&v)[W]) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < W; k += 4)
+            *reinterpret_cast<uint4*>(p + 4 * k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+    } else if constexpr (W % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < W; k += 2) *reinterpret_cast<uint2*>(p + 4 * k) = make_uint2(v[k], v[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < W; ++k) reinterpret_cast<uint32_t*>(p)[k] = v[k];
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void load_record(const uint8_t* p, uint32_t (&v)[W]) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < W; k += 4) {
+            uint4 q = *reinterpret_cast<const uint4*>(p + 4 * k);
+            v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+        }
+    } else if constexpr (W % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < W; k += 2) {
+            uint2 q = *reinterpret_cast<const uint2*>(p + 4 * k);
+            v[k] = q.x; v[k + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < W; ++k) v[k] = reinterpret_cast<const uint32_t*>(p)[k];
+    }
+}
+
+// ITER records per lane, spaced one workgroup-width apart, so every wave
+// instruction still touches consecutive elements while each lane keeps
+// ITER*W independent loads in flight.
+template <int W, int ITER>
+__global__ __launch_bounds__(kBlock) void k_pack_dword(DwordMap m, uint8_t* __restrict__ wire,
+                                                       uint64_t n) {
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
+    uint32_t v[ITER][W];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+        if (r < n) {
+#pragma unroll
+            for (int k = 0; k < W; ++k) v[it][k] = m.src[k][r << m.lg[k]];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+        if (r < n) store_record<W>(wire + r * (4 * W), v[it]);
+    }
+}
+
+template <int W, int ITER>
+__global__ __launch_bounds__(kBlock) void k_unpack_dword(DwordMap m, const uint8_t* __restrict__ wire,
+                                                         uint64_t n) {
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
+    uint32_t v[ITER][W];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+        if (r < n) load_record<W>(wire + r * (4 * W), v[it]);
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+        if (r < n) {
+#pragma unroll
+            for (int k = 0; k < W; ++k) const_cast<uint32_t*>(m.src[k])[r << m.lg[k]] = v[it][k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TILE path
+// ---------------------------------------------------------------------------
+// LDS layout (dynamic, 16-byte aligned base): image[R*stride] | tmpl[L] | mask[L]
+__device__ __forceinline__ void build_template(const TileArgs& a, uint8_t* tmpl, uint8_t* mask) {
+    for (uint32_t i = threadIdx.x; i < a.L; i += kBlock) {
+        const uint32_t pos = i % a.stride;
+        const bool pre = pos < a.prefix_len;
+        tmpl[i] = pre ? a.prefix[pos] : 0;
+        mask[i] = pre ? 0xFF : 0;
+    }
+}
+
+__device__ __forceinline__ uint4 and_not_or(uint4 v, uint4 m, uint4 t) {
+    return make_uint4((v.x & ~m.x) | t.x, (v.y & ~m.y) | t.y, (v.z & ~m.z) | t.z, (v.w & ~m.w) | t.w);
+}
+
+// Scatter the elements of one 16-byte column chunk into the tile image.
+template <int S>
+__device__ __forceinline__ void scatter_chunk(uint8_t* img, const uint4& q, uint32_t e0, uint32_t ne,
+                                              uint32_t stride, uint32_t off) {
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(&q);
+#pragma unroll
+    for (int j = 0; j < 16 / S; ++j)
+        if (static_cast<uint32_t>(j) < ne) __builtin_memcpy(img + (e0 + j) * stride + off, b + j * S, S);
+}
+
+template <int S>
+__device__ __forceinline__ uint4 gather_chunk(const uint8_t* img, uint32_t e0, uint32_t ne,
+                                              uint32_t stride, uint32_t off) {
+    uint4 q = make_uint4(0, 0, 0, 0);
+    uint8_t* b = reinterpret_cast<uint8_t*>(&q);
+#pragma unroll
+    for (int j = 0; j < 16 / S; ++j)
+        if (static_cast<uint32_t>(j) < ne) __builtin_memcpy(b + j * S, img + (e0 + j) * stride + off, S);
+    return q;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __restrict__ wire, uint64_t n,
+                                                      uint64_t ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t T = a.R * a.stride;
+    uint8_t* img = lds;
+    uint8_t* tmpl = lds + T;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) build_template(a, tmpl, mask);
+
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t rbase = tile * a.R;
+        const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+        // 1. columns -> image
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            const uint32_t s = a.size[f], lg = a.lgsize[f];
+            const uint8_t* src = a.col[f] + rbase * s;
+            const uint32_t nbytes = nr * s;
+            const uint32_t nchunks = (nbytes + 15) >> 4;
+            for (uint32_t c = threadIdx.x; c < nchunks; c += kBlock) {
+                uint4 q;
+                if ((c + 1) * 16 <= nbytes) {
+                    q = *reinterpret_cast<const uint4*>(src + 16 * c);
+                } else {
+                    q = make_uint4(0, 0, 0, 0);
+                    uint8_t* qb = reinterpret_cast<uint8_t*>(&q);
+                    for (uint32_t i = 16 * c; i < nbytes; ++i) qb[i - 16 * c] = src[i];
+                }
+                const uint32_t e0 = (16 * c) >> lg;
+                const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+                switch (s) {
+                case 1: scatter_chunk<1>(img, q, e0, ne, a.stride, a.off[f]); break;
+                case 2: scatter_chunk<2>(img, q, e0, ne, a.stride, a.off[f]); break;
+                case 4: scatter_chunk<4>(img, q, e0, ne, a.stride, a.off[f]); break;
+                default: scatter_chunk<8>(img, q, e0, ne, a.stride, a.off[f]); break;
+                }
+            }
+        }
+        __syncthreads();
+        // 2. image (+ prefix template) -> wire, 16-byte aligned stores
+        uint8_t* dst = wire + rbase * a.stride;
+        const uint32_t tbytes = nr * a.stride;
+        const uint32_t full = tbytes >> 4;
+        for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+            uint4 v = *reinterpret_cast<const uint4*>(img + 16 * c);
+            if (a.prefix_len) {
+                const uint32_t ph = (16 * c) % a.L;
+                v = and_not_or(v, *reinterpret_cast<const uint4*>(mask + ph),
+                               *reinterpret_cast<const uint4*>(tmpl + ph));
+            }
+            *reinterpret_cast<uint4*>(dst + 16 * c) = v;
+        }
+        if (threadIdx.x == 0) {
+            for (uint32_t i = full * 16; i < tbytes; ++i) {
+                const uint32_t ph = i % a.L;
+                dst[i] = a.prefix_len && mask[ph] ? tmpl[ph] : img[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_t* __restrict__ wire,
+                                                        uint64_t n, uint64_t ntiles,
+                                                        srpc_unpack_status* st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t T = a.R * a.stride;
+    uint8_t* img = lds;
+    uint8_t* tmpl = lds + T;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) build_template(a, tmpl, mask);
+    __syncthreads();
+
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t rbase = tile * a.R;
+        const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+        // 1. wire -> image, checking every prefix byte against the template
+        const uint8_t* src = wire + rbase * a.stride;
+        const uint32_t tbytes = nr * a.stride;
+        const uint32_t full = tbytes >> 4;
+        for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * c);
+            if (a.prefix_len && st) {
+                const uint32_t ph = (16 * c) % a.L;
+                const uint4 m = *reinterpret_cast<const uint4*>(mask + ph);
+                const uint4 t = *reinterpret_cast<const uint4*>(tmpl + ph);
+                if (((v.x & m.x) != t.x) | ((v.y & m.y) != t.y) | ((v.z & m.z) != t.z) |
+                    ((v.w & m.w) != t.w)) {
+                    // first record touched by a differing byte of this chunk
+                    uint32_t i = 16 * c;
+                    const uint8_t* vb = reinterpret_cast<const uint8_t*>(&v);
+                    while ((vb[i - 16 * c] & mask[(i) % a.L]) == tmpl[(i) % a.L]) ++i;
+                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                }
+            }
+            *reinterpret_cast<uint4*>(img + 16 * c) = v;
+        }
+        if (threadIdx.x == 0) {
+            for (uint32_t i = full * 16; i < tbytes; ++i) {
+                const uint8_t b = src[i];
+                const uint32_t ph = i % a.L;
+                if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph])
+                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                img[i] = b;
+            }
+        }
+        __syncthreads();
+        // 2. image -> columns
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            const uint32_t s = a.size[f], lg = a.lgsize[f];
+            uint8_t* dstc = const_cast<uint8_t*>(a.col[f]) + rbase * s;
+            const uint32_t nbytes = nr * s;
+            const uint32_t nchunks = (nbytes + 15) >> 4;
+            for (uint32_t c = threadIdx.x; c < nchunks; c += kBlock) {
+                const uint32_t e0 = (16 * c) >> lg;
+                const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+                uint4 q;
+                switch (s) {
+                case 1: q = gather_chunk<1>(img, e0, ne, a.stride, a.off[f]); break;
+                case 2: q = gather_chunk<2>(img, e0, ne, a.stride, a.off[f]); break;
+                case 4: q = gather_chunk<4>(img, e0, ne, a.stride, a.off[f]); break;
+                default: q = gather_chunk<8>(img, e0, ne, a.stride, a.off[f]); break;
+                }
+                if ((c + 1) * 16 <= nbytes) {
+                    *reinterpret_cast<uint4*>(dstc + 16 * c) = q;
+                } else {
+                    const uint8_t* qb = reinterpret_cast<const uint8_t*>(&q);
+                    for (uint32_t i = 16 * c; i < nbytes; ++i) dstc[i] = qb[i - 16 * c];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_set_status(srpc_unpack_status* st, uint32_t flags, uint64_t first_bad) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        if (flags) {
+            atomicOr(&st->flags, flags);
+            atomicMin(reinterpret_cast<unsigned long long*>(&st->first_bad_record),
+                      static_cast<unsigned long long>(first_bad));
+        } else {
+            st->flags = 0;
+            st->reserved = 0;
+            st->first_bad_record = ~0ull;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input generator (SURVEY.md §8c splitmix64)
+// ---------------------------------------------------------------------------
+struct FillArgs {
+    uint32_t* col[kMaxFields];
+};
+
+__global__ __launch_bounds__(kBlock) void k_fill_splitmix(FillArgs a, uint32_t nfields, uint64_t n,
+                                                          uint64_t seed, uint64_t first) {
+    const uint64_t gsz = static_cast<uint64_t>(gridDim.x) * kBlock;
+    for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; r < n; r += gsz) {
+        for (uint32_t f = 0; f < nfields; ++f) {
+            uint64_t z = seed + ((first + r) * nfields + f + 1) * 0x9E3779B97F4A7C15ull;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            a.col[f][r] = static_cast<uint32_t>(z);
+        }
+    }
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side: plans and the C ABI
+// ===========================================================================
+struct srpc_plan {
+    int device = 0;
+    uint32_t nfields = 0;
+    int32_t kinds[kMaxFields] = {};
+    uint32_t size[kMaxFields] = {};
+    uint32_t off[kMaxFields] = {};   // offset within record, prefix included
+    uint32_t prefix_len = 0;
+    uint8_t h_prefix[kMaxPrefix] = {};
+    uint8_t* d_prefix = nullptr;
+    uint64_t stride = 0;             // fixed record bytes (0 for string schemas)
+    bool has_string = false;
+    bool dword_ok = false;
+    int path = 0;
+    uint32_t tile_R = 0, tile_L = 0;
+    int tile_grid = 0;               // resident workgroups for grid-stride tiles
+    size_t tile_lds = 0;
+};
+
+namespace {
+
+int kind_size(int32_t k) {
+    switch (k) {
+    case SRPC_KIND_BOOL:
+    case SRPC_KIND_INT8:
+    case SRPC_KIND_CHAR: return 1;
+    case SRPC_KIND_INT16: return 2;
+    case SRPC_KIND_INT32: return 4;
+    case SRPC_KIND_INT64: return 8;
+    case SRPC_KIND_STRING: return 0;
+    default: return -1;
+    }
+}
+
+uint32_t gcd_u32(uint32_t a, uint32_t b) {
+    while (b) {
+        uint32_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+uint32_t ilog2(uint32_t s) { return s == 1 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3; }
+
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <int W>
+int launch_dword_pack(const DwordMap& m, uint8_t* wire, uint64_t n, hipStream_t s) {
+    constexpr int ITER = 4;
+    const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
+    const uint64_t grid = (n + per - 1) / per;
+    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    hipLaunchKernelGGL((k_pack_dword<W, ITER>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, m,
+                       wire, n);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+template <int W>
+int launch_dword_unpack(const DwordMap& m, const uint8_t* wire, uint64_t n, hipStream_t s) {
+    constexpr int ITER = 4;
+    const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
+    const uint64_t grid = (n + per - 1) / per;
+    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    hipLaunchKernelGGL((k_unpack_dword<W, ITER>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s,
+                       m, wire, n);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+DwordMap make_dword_map(const srpc_plan* p, const void* const* cols) {
+    DwordMap m{};
+    uint32_t k = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        const uint32_t dw = p->size[f] / 4;
+        for (uint32_t j = 0; j < dw; ++j, ++k) {
+            m.src[k] = static_cast<const uint32_t*>(cols[f]) + j;
+            m.lg[k] = dw == 2 ? 1 : 0;
+        }
+    }
+    return m;
+}
+
+TileArgs make_tile_args(const srpc_plan* p, const void* const* cols) {
+    TileArgs a{};
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        a.col[f] = static_cast<const uint8_t*>(cols[f]);
+        a.size[f] = p->size[f];
+        a.lgsize[f] = ilog2(p->size[f]);
+        a.off[f] = p->off[f];
+    }
+    a.prefix = p->d_prefix;
+    a.nfields = p->nfields;
+    a.stride = static_cast<uint32_t>(p->stride);
+    a.prefix_len = p->prefix_len;
+    a.R = p->tile_R;
+    a.L = p->tile_L;
+    return a;
+}
+
+int check_cols(const srpc_plan* p, const void* const* cols, uint64_t n) {
+    if (n == 0) return SRPC_OK;
+    if (!cols) return SRPC_E_INVALID;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (!cols[f]) return SRPC_E_INVALID;
+        const uintptr_t need = p->path == SRPC_PATH_TILE ? 16 : 4;
+        if (!aligned(cols[f], need)) return SRPC_E_ALIGN;
+    }
+    return SRPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srpc_gpu_abi_version(void) { return SRPC_GPU_ABI_VERSION; }
+
+const char* srpc_status_string(int code) {
+    switch (code) {
+    case SRPC_OK: return "ok";
+    case SRPC_E_INVALID: return "invalid argument or schema";
+    case SRPC_E_ALIGN: return "device pointer misaligned";
+    case SRPC_E_HIP: return "HIP runtime error";
+    case SRPC_E_UNSUPPORTED: return "schema not supported by this build";
+    case SRPC_E_CAPACITY: return "output buffer too small";
+    case SRPC_ERR_BOUNDS: return "wire shorter than the requested records";
+    default: return "unknown status";
+    }
+}
+
+int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
+    if (!d || !out) return SRPC_E_INVALID;
+    *out = nullptr;
+    if (d->nfields == 0 || d->nfields > static_cast<uint32_t>(kMaxFields) || !d->kinds)
+        return SRPC_E_INVALID;
+    if (d->prefix_len > kMaxPrefix || (d->prefix_len && !d->prefix)) return SRPC_E_INVALID;
+    auto* p = new (std::nothrow) srpc_plan();
+    if (!p) return SRPC_E_INVALID;
+    p->device = device;
+    p->nfields = d->nfields;
+    p->prefix_len = d->prefix_len;
+    if (d->prefix_len) std::memcpy(p->h_prefix, d->prefix, d->prefix_len);
+    uint64_t o = d->prefix_len;
+    // The DWORD path has no envelope support: prefixed schemas use TILE.
+    bool dword_ok = d->prefix_len == 0;
+    for (uint32_t f = 0; f < d->nfields; ++f) {
+        const int s = kind_size(d->kinds[f]);
+        if (s < 0) {
+            delete p;
+            return SRPC_E_INVALID;
+        }
+        p->kinds[f] = d->kinds[f];
+        p->size[f] = static_cast<uint32_t>(s);
+        p->off[f] = static_cast<uint32_t>(o);
+        if (s == 0) p->has_string = true;
+        if (s != 4 && s != 8) dword_ok = false;
+        o += static_cast<uint64_t>(s);
+    }
+    if (p->has_string) {
+        // Variable-length records are not in this build yet.
+        delete p;
+        return SRPC_E_UNSUPPORTED;
+    }
+    p->stride = o;
+    p->dword_ok = dword_ok && (o / 4) <= static_cast<uint64_t>(kMaxDwords);
+    if (o <= kMaxTileStride) {
+        const uint32_t S = static_cast<uint32_t>(o);
+        uint32_t R = 16 * std::max<uint32_t>(1, kTileTarget / (16 * S));
+        p->tile_R = R;
+        p->tile_L = S / gcd_u32(S, 16) * 16;  // lcm(S, 16)
+        p->tile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
+    }
+    p->path = p->dword_ok ? SRPC_PATH_DWORD : (p->tile_R ? SRPC_PATH_TILE : 0);
+    if (!p->path) {
+        delete p;
+        return SRPC_E_UNSUPPORTED;
+    }
+    DeviceGuard g(device);
+    if (p->prefix_len) {
+        if (hipMalloc(&p->d_prefix, p->prefix_len) != hipSuccess ||
+            hipMemcpy(p->d_prefix, p->h_prefix, p->prefix_len, hipMemcpyHostToDevice) != hipSuccess) {
+            if (p->d_prefix) (void)hipFree(p->d_prefix);
+            delete p;
+            return SRPC_E_HIP;
+        }
+    }
+    if (p->tile_R) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_tile, kBlock, p->tile_lds) !=
+                hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+            per_cu = 4;
+            cus = 256;
+        }
+        p->tile_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
+    }
+    *out = p;
+    return SRPC_OK;
+}
+
+int srpc_plan_destroy(srpc_plan* p) {
+    if (!p) return SRPC_E_INVALID;
+    if (p->d_prefix) {
+        DeviceGuard g(p->device);
+        (void)hipFree(p->d_prefix);
+    }
+    delete p;
+    return SRPC_OK;
+}
+
+int srpc_plan_record_bytes(const srpc_plan* p, uint64_t* out) {
+    if (!p || !out) return SRPC_E_INVALID;
+    *out = p->has_string ? 0 : p->stride;
+    return SRPC_OK;
+}
+
+int srpc_plan_path(const srpc_plan* p, int* out) {
+    if (!p || !out) return SRPC_E_INVALID;
+    *out = p->path;
+    return SRPC_OK;
+}
+
+int srpc_plan_force_path(srpc_plan* p, int path) {
+    if (!p) return SRPC_E_INVALID;
+    if (path == SRPC_PATH_DWORD && p->dword_ok) {
+        p->path = path;
+        return SRPC_OK;
+    }
+    if (path == SRPC_PATH_TILE && p->tile_R) {
+        p->path = path;
+        return SRPC_OK;
+    }
+    return SRPC_E_UNSUPPORTED;
+}
+
+int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8_t* wire,
+                  uint64_t wire_cap, void* stream) {
+    if (!p) return SRPC_E_INVALID;
+    if (n == 0) return SRPC_OK;
+    if (!wire) return SRPC_E_INVALID;
+    if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
+    if (!aligned(wire, 16)) return SRPC_E_ALIGN;
+    int rc = check_cols(p, cols, n);
+    if (rc) return rc;
+    auto s = static_cast<hipStream_t>(stream);
+    if (p->path == SRPC_PATH_DWORD) {
+        const DwordMap m = make_dword_map(p, cols);
+        switch (p->stride / 4) {
+        case 1: return launch_dword_pack<1>(m, wire, n, s);
+        case 2: return launch_dword_pack<2>(m, wire, n, s);
+        case 3: return launch_dword_pack<3>(m, wire, n, s);
+        case 4: return launch_dword_pack<4>(m, wire, n, s);
+        case 5: return launch_dword_pack<5>(m, wire, n, s);
+        case 6: return launch_dword_pack<6>(m, wire, n, s);
+        case 7: return launch_dword_pack<7>(m, wire, n, s);
+        case 8: return launch_dword_pack<8>(m, wire, n, s);
+        default: return SRPC_E_UNSUPPORTED;
+        }
+    }
+    const TileArgs a = make_tile_args(p, cols);
+    const uint64_t ntiles = (n + p->tile_R - 1) / p->tile_R;
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
+    hipLaunchKernelGGL(k_pack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n, ntiles);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                    void* const* cols, srpc_unpack_status* st, void* stream) {
+    if (!p) return SRPC_E_INVALID;
+    auto s = static_cast<hipStream_t>(stream);
+    if (st) {
+        hipLaunchKernelGGL(k_set_status, dim3(1), dim3(64), 0, s, st, 0u, 0ull);
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    }
+    if (n == 0) return SRPC_OK;
+    if (!wire) return SRPC_E_INVALID;
+    if (!aligned(wire, 16)) return SRPC_E_ALIGN;
+    int rc = check_cols(p, reinterpret_cast<const void* const*>(cols), n);
+    if (rc) return rc;
+    uint64_t n_fit = wire_len / p->stride;
+    int ret = SRPC_OK;
+    if (n_fit < n) {
+        if (st) {
+            hipLaunchKernelGGL(k_set_status, dim3(1), dim3(64), 0, s, st, SRPC_STATUS_BOUNDS, n_fit);
+            if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+        }
+        ret = SRPC_ERR_BOUNDS;
+    } else {
+        n_fit = n;
+    }
+    if (n_fit == 0) return ret;
+    if (p->path == SRPC_PATH_DWORD) {
+        const DwordMap m = make_dword_map(p, reinterpret_cast<const void* const*>(cols));
+        switch (p->stride / 4) {
+        case 1: rc = launch_dword_unpack<1>(m, wire, n_fit, s); break;
+        case 2: rc = launch_dword_unpack<2>(m, wire, n_fit, s); break;
+        case 3: rc = launch_dword_unpack<3>(m, wire, n_fit, s); break;
+        case 4: rc = launch_dword_unpack<4>(m, wire, n_fit, s); break;
+        case 5: rc = launch_dword_unpack<5>(m, wire, n_fit, s); break;
+        case 6: rc = launch_dword_unpack<6>(m, wire, n_fit, s); break;
+        case 7: rc = launch_dword_unpack<7>(m, wire, n_fit, s); break;
+        case 8: rc = launch_dword_unpack<8>(m, wire, n_fit, s); break;
+        default: rc = SRPC_E_UNSUPPORTED;
+        }
+        return rc ? rc : ret;
+    }
+    const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols));
+    const uint64_t ntiles = (n_fit + p->tile_R - 1) / p->tile_R;
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
+    hipLaunchKernelGGL(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
+    if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    return ret;
+}
+
+int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t* out) {
+    (void)n;
+    if (!p || !out) return SRPC_E_INVALID;
+    return SRPC_E_UNSUPPORTED;
+}
+
+int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_t* const* str_offs,
+                      uint64_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* rec_offs, void* scratch,
+                      uint64_t scratch_bytes, void* stream) {
+    (void)p; (void)cols; (void)str_offs; (void)n; (void)wire; (void)wire_cap; (void)rec_offs;
+    (void)scratch; (void)scratch_bytes; (void)stream;
+    return SRPC_E_UNSUPPORTED;
+}
+
+int srpc_gpu_fill_splitmix_i32(int32_t* const* cols, uint32_t nfields, uint64_t n, uint64_t seed,
+                               uint64_t first_record, void* stream) {
+    if (nfields == 0 || nfields > static_cast<uint32_t>(kMaxFields) || !cols) return SRPC_E_INVALID;
+    if (n == 0) return SRPC_OK;
+    FillArgs a{};
+    for (uint32_t f = 0; f < nfields; ++f) {
+        if (!cols[f]) return SRPC_E_INVALID;
+        a.col[f] = reinterpret_cast<uint32_t*>(cols[f]);
+    }
+    const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_fill_splitmix, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), a, nfields, n, seed, first_record);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+}  // extern "C"

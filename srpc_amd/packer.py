@@ -1,0 +1,182 @@
+"""Host-side batch packer over the HIP C ABI.
+
+Mirrors the reference packer's vocabulary (include/srpc/packer.hpp):
+``pack`` / ``unpack`` are the batched ``p << r`` / ``r.unpack(bp)`` loops,
+``for_request`` / ``for_response`` build the constant envelope header that
+``packer::pack_request`` (packer.hpp:77-82) and ``packer::pack_response``
+(packer.hpp:86-91) emit in front of every body.
+
+Device memory is passed as raw device pointers (ints) or as any object with a
+``data_ptr()`` method (e.g. a torch tensor on the GPU); streams as a raw
+``hipStream_t`` (int) or an object with ``cuda_stream``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from dataclasses import dataclass, field
+from typing import Iterable, Sequence
+
+from . import _lib
+from ._lib import SrpcError, check
+
+# IDL kinds (include/srpc_gpu.h, = the type table of parser.hpp:253-290)
+BOOL, INT8, CHAR, INT16, INT32, INT64, STRING = 1, 2, 3, 4, 5, 6, 7
+KIND_NAMES = {"bool": BOOL, "int8": INT8, "char": CHAR, "int16": INT16, "int32": INT32,
+              "int64": INT64, "string": STRING}
+KIND_SIZE = {BOOL: 1, INT8: 1, CHAR: 1, INT16: 2, INT32: 4, INT64: 8, STRING: 0}
+
+# rpc_status_code (packer.hpp:16-20)
+RPC_SUCCESS, RPC_ERR_FUNCTION_NOT_REGISTERED, RPC_ERR_RECV_TIMEOUT = 0, 1, 2
+
+
+@dataclass(frozen=True)
+class Schema:
+    """A message type: its name (``T::name``) and its flattened fields in
+    ``T::fields`` declaration order (nested messages inlined, as
+    ``pack_arg`` does for message-typed members, packer.hpp:185-186)."""
+
+    name: str
+    fields: tuple = field(default_factory=tuple)  # ((field_name, kind), ...)
+
+    @staticmethod
+    def of(name: str, *fields) -> "Schema":
+        out = []
+        for fname, kind in fields:
+            if isinstance(kind, Schema):  # nested message: inline its fields
+                out.extend((f"{fname}.{n}", k) for n, k in kind.fields)
+            else:
+                out.append((fname, KIND_NAMES[kind] if isinstance(kind, str) else int(kind)))
+        return Schema(name, tuple(out))
+
+    @property
+    def kinds(self) -> list[int]:
+        return [k for _, k in self.fields]
+
+    @property
+    def body_bytes(self) -> int:
+        """Fixed body size, 0 if the schema has a string field."""
+        if any(k == STRING for k in self.kinds):
+            return 0
+        return sum(KIND_SIZE[k] for k in self.kinds)
+
+
+def request_prefix(method: str, msg_name: str) -> bytes:
+    """``u64 len(method) | method | u64 len(T::name) | T::name`` (packer.hpp:77-82,
+    strings per pack_arg<std::string> 193-198 and pack_arg<const char*> 203-208)."""
+    m, n = method.encode(), msg_name.encode()
+    return struct.pack("<Q", len(m)) + m + struct.pack("<Q", len(n)) + n
+
+
+def response_prefix(code: int, msg_name: str) -> bytes:
+    """``u8 code | u64 len(T::name) | T::name`` (packer.hpp:86-91)."""
+    n = msg_name.encode()
+    return bytes([code & 0xFF]) + struct.pack("<Q", len(n)) + n
+
+
+def _dptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    raise TypeError(f"expected a device pointer or tensor, got {type(x)!r}")
+
+
+def _stream(s) -> int:
+    if s is None:
+        return 0
+    if isinstance(s, int):
+        return s
+    if hasattr(s, "cuda_stream"):
+        return int(s.cuda_stream)
+    raise TypeError(f"expected a hipStream_t handle or stream object, got {type(s)!r}")
+
+
+class GpuPacker:
+    """A plan for one record schema (+ optional envelope prefix) on one device."""
+
+    def __init__(self, schema: Schema, prefix: bytes = b"", device: int = 0):
+        self.schema = schema
+        self.prefix = bytes(prefix)
+        self.device = device
+        L = _lib.lib()
+        kinds = (C.c_int32 * len(schema.kinds))(*schema.kinds)
+        pre = (C.c_uint8 * max(1, len(self.prefix))).from_buffer_copy(self.prefix or b"\0")
+        desc = _lib.SchemaDesc(len(schema.kinds), kinds, pre, len(self.prefix))
+        h = C.c_void_p()
+        check(L.srpc_plan_create(C.byref(desc), device, C.byref(h)), "srpc_plan_create")
+        self._h = h
+        rb = C.c_uint64()
+        check(L.srpc_plan_record_bytes(h, C.byref(rb)), "srpc_plan_record_bytes")
+        self.record_bytes = rb.value
+
+    @classmethod
+    def for_request(cls, schema: Schema, method: str, device: int = 0) -> "GpuPacker":
+        return cls(schema, request_prefix(method, schema.name), device)
+
+    @classmethod
+    def for_response(cls, schema: Schema, code: int = RPC_SUCCESS, device: int = 0) -> "GpuPacker":
+        return cls(schema, response_prefix(code, schema.name), device)
+
+    # -- plan info ---------------------------------------------------------
+    @property
+    def path(self) -> int:
+        p = C.c_int()
+        check(_lib.lib().srpc_plan_path(self._h, C.byref(p)), "srpc_plan_path")
+        return p.value
+
+    def force_path(self, path: int) -> None:
+        check(_lib.lib().srpc_plan_force_path(self._h, path), "srpc_plan_force_path")
+
+    def wire_bytes(self, n: int) -> int:
+        return n * self.record_bytes
+
+    # -- hot path ----------------------------------------------------------
+    def _cols(self, cols: Sequence) -> C.Array:
+        if len(cols) != len(self.schema.kinds):
+            raise ValueError(f"{self.schema.name}: expected {len(self.schema.kinds)} columns, "
+                             f"got {len(cols)}")
+        return (C.c_void_p * len(cols))(*[_dptr(c) for c in cols])
+
+    def pack(self, cols: Sequence, n: int, wire, wire_cap: int | None = None, stream=None) -> int:
+        """Pack n records from device columns into device wire bytes (async)."""
+        arr = self._cols(cols)
+        cap = self.wire_bytes(n) if wire_cap is None else wire_cap
+        check(_lib.lib().srpc_gpu_pack(self._h, arr, n, _dptr(wire), cap, _stream(stream)),
+              "srpc_gpu_pack")
+        return self.wire_bytes(n)
+
+    def unpack(self, wire, wire_len: int, n: int, cols: Sequence, status=None, stream=None) -> int:
+        """Unpack n records from device wire bytes into device columns (async).
+        ``status``: device pointer to a 16-byte srpc_unpack_status, or None.
+        Returns SRPC_OK or SRPC_ERR_BOUNDS."""
+        arr = self._cols(cols)
+        return check(_lib.lib().srpc_gpu_unpack(self._h, _dptr(wire), wire_len, n, arr,
+                                                _dptr(status), _stream(stream)),
+                     "srpc_gpu_unpack")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().srpc_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fill_splitmix_i32(cols: Iterable, n: int, seed: int, first_record: int = 0, stream=None) -> None:
+    """Synthetic int32 columns on the device (SURVEY.md §8c splitmix64 stream)."""
+    ptrs = [_dptr(c) for c in cols]
+    arr = (C.c_void_p * len(ptrs))(*ptrs)
+    check(_lib.lib().srpc_gpu_fill_splitmix_i32(arr, len(ptrs), n, seed, first_record,
+                                                _stream(stream)), "srpc_gpu_fill_splitmix_i32")
+
+
+__all__ = ["Schema", "GpuPacker", "SrpcError", "request_prefix", "response_prefix",
+           "fill_splitmix_i32", "BOOL", "INT8", "CHAR", "INT16", "INT32", "INT64", "STRING",
+           "RPC_SUCCESS", "RPC_ERR_FUNCTION_NOT_REGISTERED", "RPC_ERR_RECV_TIMEOUT"]

@@ -1,0 +1,282 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and the
+reference-produced fixtures.  Bit-exact: this is byte/integer work.
+
+Small cases run against oracle/packer_oracle.c on the same seeded inputs;
+full BASELINE.json sizes are checked against the reference's SHA-256 digests
+(tests/golden/manifest.json) and by pack -> unpack round trips.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import srpc_amd
+from srpc_amd import (NUMBER, QUAD, SQUARE_METHOD, TWO_NUMBERS, GpuPacker, Schema,
+                      SRPC_ERR_BOUNDS, SRPC_PATH_DWORD, SRPC_PATH_TILE, SRPC_STATUS_BOUNDS,
+                      SRPC_STATUS_PREFIX)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+
+
+def dev(a: np.ndarray) -> "torch.Tensor":
+    """numpy -> device tensor with the same bytes (16-byte aligned allocation)."""
+    b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    t = torch.empty(max(b.size, 1), dtype=torch.uint8, device=DEV)
+    if b.size:
+        t[: b.size].copy_(torch.from_numpy(b.copy()))
+    return t
+
+
+def host(t, nbytes: int, dtype=np.uint8) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t[:nbytes].cpu().numpy().view(dtype) if nbytes else np.zeros(0, dtype)
+
+
+def empty(nbytes: int):
+    return torch.full((max(nbytes, 1),), 0xA5, dtype=torch.uint8, device=DEV)
+
+
+def status_buf():
+    return torch.zeros(16, dtype=torch.uint8, device=DEV)
+
+
+def read_status(t):
+    b = host(t, 16)
+    flags = int(b[:4].view(np.uint32)[0])
+    first = int(b[8:16].view(np.uint64)[0])
+    return flags, first
+
+
+def gpu_pack(packer, cols, n):
+    dcols = [dev(c) for c in cols]
+    wire = empty(packer.wire_bytes(n))
+    packer.pack(dcols, n, wire)
+    return host(wire, packer.wire_bytes(n)).tobytes()
+
+
+def gpu_unpack(packer, wire: bytes, n, dtypes, wire_len=None, status=None):
+    w = dev(np.frombuffer(wire, np.uint8)) if len(wire) else empty(16)
+    outs = [empty(n * np.dtype(dt).itemsize + 16) for dt in dtypes]
+    rc = packer.unpack(w, len(wire) if wire_len is None else wire_len, n, outs, status)
+    return rc, [host(o, n * np.dtype(dt).itemsize, dt) for o, dt in zip(outs, dtypes)]
+
+
+def read(golden_dir, name):
+    with open(os.path.join(golden_dir, name), "rb") as f:
+        return f.read()
+
+
+SIZES = [0, 1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 4096 + 17, 100_003]
+
+
+@pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
+@pytest.mark.parametrize("n", SIZES)
+def test_quad_pack_unpack_vs_oracle(n, path):
+    p = GpuPacker(QUAD)
+    assert p.path == SRPC_PATH_DWORD
+    p.force_path(path)
+    cols = oracle.splitmix_columns_i32(4, n)
+    wire = gpu_pack(p, cols, n)
+    assert wire == oracle.pack([oracle.INT32] * 4, cols, n)
+    rc, back = gpu_unpack(p, wire, n, [np.int32] * 4)
+    assert rc == 0
+    for a, b in zip(cols, back):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
+def test_quad_golden_head_and_edges(golden_dir, path):
+    p = GpuPacker(QUAD)
+    p.force_path(path)
+    cols = oracle.splitmix_columns_i32(4, 4096)
+    assert gpu_pack(p, cols, 4096) == read(golden_dir, "quad_body_head4096.bin")
+    z = np.load(os.path.join(golden_dir, "quad_edges_in.npz"))
+    ecols = [z[k] for k in "abcd"]
+    wire = read(golden_dir, "quad_edges.bin")
+    assert gpu_pack(p, ecols, 256) == wire
+    rc, back = gpu_unpack(p, wire, 256, [np.int32] * 4)
+    assert rc == 0 and all(np.array_equal(a, b) for a, b in zip(ecols, back))
+
+
+@pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
+def test_number_and_two_numbers(golden_dir, manifest, path):
+    p = GpuPacker(NUMBER)
+    p.force_path(path)
+    n = manifest["streams"]["number_body_1M"]["records"]
+    num = oracle.splitmix_columns_i32(1, n)
+    wire = gpu_pack(p, num, n)
+    assert wire[: 4096 * 4] == read(golden_dir, "number_body_head4096.bin")
+    assert hashlib.sha256(wire).hexdigest() == manifest["streams"]["number_body_1M"]["sha256"]
+    rc, back = gpu_unpack(p, wire, n, [np.int32])
+    assert rc == 0 and np.array_equal(back[0], num[0])
+    p2 = GpuPacker(TWO_NUMBERS)
+    p2.force_path(path)
+    l, r = oracle.splitmix_columns_i32(2, 1000, seed=oracle.SEED + 1)
+    assert gpu_pack(p2, [l, r], 1000) == read(golden_dir, "two_numbers.bin")
+
+
+ALL_KINDS = Schema.of("all_kinds", ("k_bool", "bool"), ("k_i8", "int8"), ("k_char", "char"),
+                      ("k_i16", "int16"), ("k_i32", "int32"), ("k_i64", "int64"))
+ALL_DT = [np.uint8, np.int8, np.int8, np.int16, np.int32, np.int64]
+
+
+def test_all_kinds_tile(golden_dir):
+    p = GpuPacker(ALL_KINDS)
+    assert p.path == SRPC_PATH_TILE and p.record_bytes == 17
+    z = np.load(os.path.join(golden_dir, "all_kinds_in.npz"))
+    cols = [z[k] for k in ("kb", "k8", "kc", "k16", "k32", "k64")]
+    wire = read(golden_dir, "all_kinds.bin")
+    assert gpu_pack(p, cols, 1000) == wire
+    rc, back = gpu_unpack(p, wire, 1000, ALL_DT)
+    assert rc == 0
+    for a, b in zip(cols, back):
+        assert a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 7, 16, 17, 333, 4099, 65537])
+@pytest.mark.parametrize("schema", ["all", "i16x3", "i64x2", "i8", "mixed_dword"])
+def test_random_schemas_vs_oracle(n, schema):
+    kinds = {"all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
+             "i16x3": [oracle.INT16] * 3, "i64x2": [oracle.INT64] * 2, "i8": [oracle.INT8],
+             "mixed_dword": [oracle.INT64, oracle.INT32, oracle.INT64]}[schema]
+    rng = np.random.default_rng(n * 31 + len(kinds))
+    cols = []
+    for k in kinds:
+        dt = np.dtype(oracle.KIND_DTYPE[k])
+        c = rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt)
+        if k == oracle.BOOL:
+            c = (c & 1).astype(np.uint8)
+        cols.append(c)
+    p = GpuPacker(Schema("X", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    paths = [p.path] + ([SRPC_PATH_TILE] if p.path == SRPC_PATH_DWORD else [])
+    want = oracle.pack(kinds, cols, n)
+    for path in paths:
+        p.force_path(path)
+        assert gpu_pack(p, cols, n) == want
+        rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+        assert rc == 0
+        for a, b in zip(cols, back):
+            assert a.tobytes() == b.tobytes()
+
+
+# ---- envelopes (Calculator.square) ---------------------------------------------
+
+def test_square_request_envelope(golden_dir, manifest):
+    st = manifest["streams"]["square_requests_1M"]
+    n = st["records"]
+    p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
+    assert p.record_bytes == 53 and p.path == SRPC_PATH_TILE
+    nums = oracle.square_inputs(n)
+    wire = gpu_pack(p, [nums], n)
+    assert wire[: 1024 * 53] == read(golden_dir, "square_req_head1024.bin")
+    assert hashlib.sha256(wire).hexdigest() == st["sha256"]
+    s = status_buf()
+    rc, back = gpu_unpack(p, wire, n, [np.int32], status=s)
+    assert rc == 0 and np.array_equal(back[0], nums)
+    assert read_status(s) == (0, 2**64 - 1)
+
+
+def test_square_response_envelope(golden_dir, manifest):
+    st = manifest["streams"]["square_responses_1M"]
+    n = st["records"]
+    p = GpuPacker.for_response(NUMBER, srpc_amd.RPC_SUCCESS)
+    assert p.record_bytes == 19
+    sq = (oracle.square_inputs(n).astype(np.int64) ** 2).astype(np.int32)
+    wire = gpu_pack(p, [sq], n)
+    assert wire[: 1024 * 19] == read(golden_dir, "square_resp_head1024.bin")
+    assert hashlib.sha256(wire).hexdigest() == st["sha256"]
+
+
+@pytest.mark.parametrize("bad", [0, 5, 143, 144, 145, 9999])
+def test_request_prefix_mismatch_reported(bad):
+    n = 10_000
+    p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
+    nums = np.arange(n, dtype=np.int32) - 5000
+    pre = oracle.request_prefix(SQUARE_METHOD, "Number")
+    wire = bytearray(oracle.pack([oracle.INT32], [nums], n, pre))
+    wire[bad * 53 + 20] ^= 0x20          # corrupt the method name of record `bad`
+    wire[min(n - 1, bad + 3) * 53 + 48] ^= 1   # and the message name of a later one
+    s = status_buf()
+    rc, back = gpu_unpack(p, bytes(wire), n, [np.int32], status=s)
+    assert rc == 0
+    flags, first = read_status(s)
+    assert flags == SRPC_STATUS_PREFIX and first == bad
+    # the oracle agrees on where decoding fails
+    st, _, _, _, err = oracle.unpack([oracle.INT32], bytes(wire), n, pre)
+    assert st == oracle.ORC_ERR_PREFIX and err == bad
+    # fields are still decoded from their fixed positions
+    assert np.array_equal(back[0], nums)
+
+
+def test_truncated_wire_bounds():
+    n = 1000
+    p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
+    nums = np.arange(n, dtype=np.int32)
+    pre = oracle.request_prefix(SQUARE_METHOD, "Number")
+    wire = oracle.pack([oracle.INT32], [nums], n, pre)
+    s = status_buf()
+    cut = len(wire) - 30
+    rc, back = gpu_unpack(p, wire[:cut], n, [np.int32], status=s)
+    assert rc == SRPC_ERR_BOUNDS
+    flags, first = read_status(s)
+    assert flags == SRPC_STATUS_BOUNDS and first == n - 1
+    assert np.array_equal(back[0][: n - 1], nums[: n - 1])
+    st, _, _, _, err = oracle.unpack([oracle.INT32], wire[:cut], n, pre)
+    assert st == oracle.ORC_ERR_BOUNDS and err == n - 1
+
+
+def test_alignment_and_capacity_errors():
+    p = GpuPacker(QUAD)
+    cols = [torch.zeros(64, dtype=torch.int32, device=DEV) for _ in range(4)]
+    wire = torch.zeros(1024 + 16, dtype=torch.uint8, device=DEV)
+    with pytest.raises(srpc_amd.SrpcError) as e:
+        p.pack(cols, 64, wire[1:].data_ptr(), 1024)
+    assert e.value.code == -2
+    with pytest.raises(srpc_amd.SrpcError) as e:
+        p.pack(cols, 64, wire, 1000)
+    assert e.value.code == -5
+
+
+def test_fill_splitmix_matches_numpy():
+    n = 100_000
+    cols = [torch.empty(n, dtype=torch.int32, device=DEV) for _ in range(4)]
+    srpc_amd.fill_splitmix_i32(cols, n, oracle.SEED, first_record=12345)
+    torch.cuda.synchronize()
+    want = oracle.splitmix_columns_i32(4, n, first_record=12345)
+    for c, w in zip(cols, want):
+        assert np.array_equal(c.cpu().numpy(), w)
+
+
+# ---- full BASELINE.json sizes ----------------------------------------------------
+
+@pytest.mark.slow
+@pytest.mark.parametrize("label", ["quad_body_16M", "quad_body_64M"])
+def test_quad_full_size_digest_and_roundtrip(manifest, label):
+    st = manifest["streams"][label]
+    n = st["records"]
+    p = GpuPacker(QUAD)
+    cols = [torch.empty(n, dtype=torch.int32, device=DEV) for _ in range(4)]
+    srpc_amd.fill_splitmix_i32(cols, n, oracle.SEED)
+    wire = torch.empty(n * 16, dtype=torch.uint8, device=DEV)
+    p.pack(cols, n, wire)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(wire.cpu().numpy().tobytes()).hexdigest() == st["sha256"]
+    back = [torch.empty(n, dtype=torch.int32, device=DEV) for _ in range(4)]
+    p.unpack(wire, n * 16, n, back)
+    torch.cuda.synchronize()
+    for a, b in zip(cols, back):
+        assert torch.equal(a, b)
+    # the TILE path produces the same bytes at full size
+    p.force_path(SRPC_PATH_TILE)
+    wire2 = torch.empty_like(wire)
+    p.pack(cols, n, wire2)
+    torch.cuda.synchronize()
+    assert torch.equal(wire, wire2)
