@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--path", choices=["auto", "dword", "tile"], default="auto")
+    ap.add_argument("--tune", default=None,
+                    help="DWORD-path variant rpl,iter,nt (default: the library's tuned default)")
     return ap.parse_args()
 
 
@@ -129,6 +131,9 @@ def main() -> None:
     p = GpuPacker(QUAD, device=local)
     if args.path != "auto":
         p.force_path({"dword": srpc_amd.SRPC_PATH_DWORD, "tile": srpc_amd.SRPC_PATH_TILE}[args.path])
+    if args.tune:
+        rpl, it, nt = (int(x) for x in args.tune.split(","))
+        p.tune(rpl, it, nt)
     stream = torch.cuda.current_stream(dev)
     cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
     back = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
@@ -239,7 +244,7 @@ def main() -> None:
 
     if rank == 0:
         total_recs = n * world
-        value = total_recs * REC_BYTES / 2**30 / (t_max)  * K
+        value = total_recs * K * REC_BYTES / 2**30 / t_max  # wire GiB/s, all ranks
         dom_name, dom_ms = ("pack", pack_avg) if pack_avg >= unpack_avg else ("unpack", unpack_avg)
         achieved = ALG_BYTES_PER_REC * n / (dom_ms / 1e3) / 1e9
         traffic = None
@@ -266,7 +271,8 @@ def main() -> None:
             "config": {"workload": "Quad{4 x int32} pack+unpack, 16-byte records, device-resident",
                        "records_per_gpu": n, "global_records": total_recs,
                        "record_bytes": REC_BYTES, "parallelism": f"shard{world}",
-                       "kernel_path": {1: "dword", 2: "tile"}[p.path]},
+                       "kernel_path": {1: "dword", 2: "tile"}[p.path],
+                       "tune": args.tune or "default"},
             "mrecords_per_s": round(total_recs * K / t_max / 1e6, 1),
             "hbm_algorithmic_GBps": round(2 * ALG_BYTES_PER_REC * total_recs * K / t_max / 1e9, 1),
             "kernels_ms": {"pack": round(pack_avg, 4), "unpack": round(unpack_avg, 4)},

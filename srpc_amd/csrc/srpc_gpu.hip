@@ -51,6 +51,8 @@ struct DwordMap {
     uint32_t lg[kMaxDwords];
 };
 
+
+
 struct TileArgs {
     const uint8_t* col[kMaxFields];  // field column base (pack: src, unpack: dst)
     uint32_t size[kMaxFields];       // field bytes: 1, 2, 4 or 8
@@ -73,45 +75,77 @@ __device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag
 // ---------------------------------------------------------------------------
 // DWORD path
 // ---------------------------------------------------------------------------
-template <int W>
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Variant bits (srpc_plan_tune SRPC_TUNE_NT): non-temporal stores / loads.
+constexpr int kNtStore = 1;
+constexpr int kNtLoad = 2;
+
+// DWORD-path variant: records per lane (1 or 4), iterations per lane, NT bits.
+// Default = the fastest in the steady-state bench loop on MI355X (16M Quad,
+// profiles/r01_tune.log): one record per lane, one iteration, non-temporal
+// loads and stores (streamed bytes are touched once per kernel).
+struct DwordVariant {
+    int rpl = 1;
+    int iter = 1;
+    int nt = kNtStore | kNtLoad;
+};
+
+template <int NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (NT & kNtLoad) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int NT, typename T>
+__device__ __forceinline__ void st(T* p, T v) {
+    if constexpr (NT & kNtStore) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// W dwords of one record to/from its (4W-byte aligned) wire slot, using the
+// widest vector the record alignment allows.
+template <int W, int NT>
 __device__ __forceinline__ void store_record(uint8_t* p, const uint32_t (&v)[W]) {
     if constexpr (W % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < W; k += 4)
-            *reinterpret_cast<uint4*>(p + 4 * k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+            st<NT>(reinterpret_cast<u32x4*>(p + 4 * k), u32x4{v[k], v[k + 1], v[k + 2], v[k + 3]});
     } else if constexpr (W % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < W; k += 2) *reinterpret_cast<uint2*>(p + 4 * k) = make_uint2(v[k], v[k + 1]);
+        for (int k = 0; k < W; k += 2) st<NT>(reinterpret_cast<u32x2*>(p + 4 * k), u32x2{v[k], v[k + 1]});
     } else {
 #pragma unroll
-        for (int k = 0; k < W; ++k) reinterpret_cast<uint32_t*>(p)[k] = v[k];
+        for (int k = 0; k < W; ++k) st<NT>(reinterpret_cast<uint32_t*>(p) + k, v[k]);
     }
 }
 
-template <int W>
+template <int W, int NT>
 __device__ __forceinline__ void load_record(const uint8_t* p, uint32_t (&v)[W]) {
     if constexpr (W % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < W; k += 4) {
-            uint4 q = *reinterpret_cast<const uint4*>(p + 4 * k);
+            const u32x4 q = ld<NT>(reinterpret_cast<const u32x4*>(p + 4 * k));
             v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
         }
     } else if constexpr (W % 2 == 0) {
 #pragma unroll
         for (int k = 0; k < W; k += 2) {
-            uint2 q = *reinterpret_cast<const uint2*>(p + 4 * k);
+            const u32x2 q = ld<NT>(reinterpret_cast<const u32x2*>(p + 4 * k));
             v[k] = q.x; v[k + 1] = q.y;
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < W; ++k) v[k] = reinterpret_cast<const uint32_t*>(p)[k];
+        for (int k = 0; k < W; ++k) v[k] = ld<NT>(reinterpret_cast<const uint32_t*>(p) + k);
     }
 }
 
-// ITER records per lane, spaced one workgroup-width apart, so every wave
-// instruction still touches consecutive elements while each lane keeps
-// ITER*W independent loads in flight.
-template <int W, int ITER>
+// One record per lane.  ITER records per lane, spaced one workgroup-width
+// apart, so every wave instruction touches consecutive elements (256 B per
+// column load, 64*4W B per record store) while each lane keeps ITER*W
+// independent loads in flight.
+template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_pack_dword(DwordMap m, uint8_t* __restrict__ wire,
                                                        uint64_t n) {
     const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
@@ -121,17 +155,17 @@ __global__ __launch_bounds__(kBlock) void k_pack_dword(DwordMap m, uint8_t* __re
         const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
         if (r < n) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) v[it][k] = m.src[k][r << m.lg[k]];
+            for (int k = 0; k < W; ++k) v[it][k] = ld<NT>(m.src[k] + (r << m.lg[k]));
         }
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
         const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) store_record<W>(wire + r * (4 * W), v[it]);
+        if (r < n) store_record<W, NT>(wire + r * (4 * W), v[it]);
     }
 }
 
-template <int W, int ITER>
+template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_unpack_dword(DwordMap m, const uint8_t* __restrict__ wire,
                                                          uint64_t n) {
     const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
@@ -139,14 +173,79 @@ __global__ __launch_bounds__(kBlock) void k_unpack_dword(DwordMap m, const uint8
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
         const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) load_record<W>(wire + r * (4 * W), v[it]);
+        if (r < n) load_record<W, NT>(wire + r * (4 * W), v[it]);
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
         const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
         if (r < n) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) const_cast<uint32_t*>(m.src[k])[r << m.lg[k]] = v[it][k];
+            for (int k = 0; k < W; ++k) st<NT>(const_cast<uint32_t*>(m.src[k]) + (r << m.lg[k]), v[it][k]);
+        }
+    }
+}
+
+// Four consecutive records per lane (all fields 4 bytes, 16-byte aligned
+// columns): one 16-byte load per column, a register transpose, and W 16-byte
+// stores of the lane's 4 contiguous records.  Records past n are handled by
+// the one-record-per-lane kernel of the same variant (the host splits n).
+template <int W, int ITER, int NT>
+__global__ __launch_bounds__(kBlock) void k_pack_dword_x4(DwordMap m, uint8_t* __restrict__ wire,
+                                                          uint64_t nq) {
+    const uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
+    u32x4 c[ITER][W];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+        if (q < nq) {
+#pragma unroll
+            for (int k = 0; k < W; ++k) c[it][k] = ld<NT>(reinterpret_cast<const u32x4*>(m.src[k]) + q);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+        if (q < nq) {
+            uint32_t o[4 * W];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int k = 0; k < W; ++k) o[i * W + k] = c[it][k][i];
+            u32x4* dst = reinterpret_cast<u32x4*>(wire + q * (16 * W));
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                st<NT>(dst + j, u32x4{o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]});
+        }
+    }
+}
+
+template <int W, int ITER, int NT>
+__global__ __launch_bounds__(kBlock) void k_unpack_dword_x4(DwordMap m, const uint8_t* __restrict__ wire,
+                                                            uint64_t nq) {
+    const uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
+    u32x4 c[ITER][W];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+        if (q < nq) {
+            const u32x4* src = reinterpret_cast<const u32x4*>(wire + q * (16 * W));
+#pragma unroll
+            for (int j = 0; j < W; ++j) c[it][j] = ld<NT>(src + j);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+        if (q < nq) {
+            uint32_t o[4 * W];
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[4 * j + e] = c[it][j][e];
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                st<NT>(reinterpret_cast<u32x4*>(const_cast<uint32_t*>(m.src[k])) + q,
+                       u32x4{o[k], o[W + k], o[2 * W + k], o[3 * W + k]});
         }
     }
 }
@@ -379,6 +478,8 @@ struct srpc_plan {
     uint32_t tile_R = 0, tile_L = 0;
     int tile_grid = 0;               // resident workgroups for grid-stride tiles
     size_t tile_lds = 0;
+    bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
+    DwordVariant dv;                 // DWORD-path variant (srpc_plan_tune)
 };
 
 namespace {
@@ -421,26 +522,80 @@ struct DeviceGuard {
     }
 };
 
-template <int W>
-int launch_dword_pack(const DwordMap& m, uint8_t* wire, uint64_t n, hipStream_t s) {
-    constexpr int ITER = 4;
+template <int W, int ITER, int NT>
+int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, hipStream_t s) {
     const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
-    const uint64_t grid = (n + per - 1) / per;
-    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    hipLaunchKernelGGL((k_pack_dword<W, ITER>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, m,
-                       wire, n);
+    uint64_t done = 0;
+    if (rpl == 4) {
+        const uint64_t nq = n / 4;
+        if (nq) {
+            const uint64_t grid = (nq + per - 1) / per;
+            if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+            if (pack)
+                hipLaunchKernelGGL((k_pack_dword_x4<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)),
+                                   dim3(kBlock), 0, s, m, wire, nq);
+            else
+                hipLaunchKernelGGL((k_unpack_dword_x4<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)),
+                                   dim3(kBlock), 0, s, m, wire, nq);
+            done = nq * 4;
+        }
+    }
+    if (done < n) {
+        // remaining records (all of them for rpl == 1): shift the map to `done`
+        DwordMap t = m;
+        for (int k = 0; k < W; ++k) t.src[k] += done << t.lg[k];
+        const uint64_t rest = n - done;
+        const uint64_t grid = (rest + per - 1) / per;
+        if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        if (pack)
+            hipLaunchKernelGGL((k_pack_dword<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                               0, s, t, wire + done * 4 * W, rest);
+        else
+            hipLaunchKernelGGL((k_unpack_dword<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                               0, s, t, wire + done * 4 * W, rest);
+    }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
+// Tuning matrix (ITER x NT) is instantiated only for the record widths that
+// matter for throughput (Number, TwoNumbers, Quad); other widths run the
+// default variant.
 template <int W>
-int launch_dword_unpack(const DwordMap& m, const uint8_t* wire, uint64_t n, hipStream_t s) {
-    constexpr int ITER = 4;
-    const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
-    const uint64_t grid = (n + per - 1) / per;
-    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    hipLaunchKernelGGL((k_unpack_dword<W, ITER>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s,
-                       m, wire, n);
-    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+int launch_dword(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, const DwordVariant& v,
+                 hipStream_t s) {
+    if constexpr (W == 1 || W == 2 || W == 4) {
+#define SRPC_NT_CASES(IT)                                                        \
+    switch (v.nt) {                                                              \
+    case 0: return launch_dword_v<W, IT, 0>(pack, m, wire, n, v.rpl, s);         \
+    case 1: return launch_dword_v<W, IT, 1>(pack, m, wire, n, v.rpl, s);         \
+    case 2: return launch_dword_v<W, IT, 2>(pack, m, wire, n, v.rpl, s);         \
+    default: return launch_dword_v<W, IT, 3>(pack, m, wire, n, v.rpl, s);        \
+    }
+        switch (v.iter) {
+        case 1: SRPC_NT_CASES(1)
+        case 2: SRPC_NT_CASES(2)
+        case 8: SRPC_NT_CASES(8)
+        default: SRPC_NT_CASES(4)
+        }
+#undef SRPC_NT_CASES
+    } else {
+        return launch_dword_v<W, 4, 0>(pack, m, wire, n, 1, s);
+    }
+}
+
+int launch_dword_any(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, uint32_t W,
+                     const DwordVariant& v, hipStream_t s) {
+    switch (W) {
+    case 1: return launch_dword<1>(pack, m, wire, n, v, s);
+    case 2: return launch_dword<2>(pack, m, wire, n, v, s);
+    case 3: return launch_dword<3>(pack, m, wire, n, v, s);
+    case 4: return launch_dword<4>(pack, m, wire, n, v, s);
+    case 5: return launch_dword<5>(pack, m, wire, n, v, s);
+    case 6: return launch_dword<6>(pack, m, wire, n, v, s);
+    case 7: return launch_dword<7>(pack, m, wire, n, v, s);
+    case 8: return launch_dword<8>(pack, m, wire, n, v, s);
+    default: return SRPC_E_UNSUPPORTED;
+    }
 }
 
 DwordMap make_dword_map(const srpc_plan* p, const void* const* cols) {
@@ -471,6 +626,12 @@ TileArgs make_tile_args(const srpc_plan* p, const void* const* cols) {
     a.R = p->tile_R;
     a.L = p->tile_L;
     return a;
+}
+
+bool check_cols_aligned(const void* const* cols, uint32_t nf, uintptr_t a) {
+    for (uint32_t f = 0; f < nf; ++f)
+        if (!aligned(cols[f], a)) return false;
+    return true;
 }
 
 int check_cols(const srpc_plan* p, const void* const* cols, uint64_t n) {
@@ -518,6 +679,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
     uint64_t o = d->prefix_len;
     // The DWORD path has no envelope support: prefixed schemas use TILE.
     bool dword_ok = d->prefix_len == 0;
+    bool all4_fields = true;
     for (uint32_t f = 0; f < d->nfields; ++f) {
         const int s = kind_size(d->kinds[f]);
         if (s < 0) {
@@ -529,6 +691,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         p->off[f] = static_cast<uint32_t>(o);
         if (s == 0) p->has_string = true;
         if (s != 4 && s != 8) dword_ok = false;
+        if (s != 4) all4_fields = false;
         o += static_cast<uint64_t>(s);
     }
     if (p->has_string) {
@@ -537,6 +700,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         return SRPC_E_UNSUPPORTED;
     }
     p->stride = o;
+    p->all4 = all4_fields;
     p->dword_ok = dword_ok && (o / 4) <= static_cast<uint64_t>(kMaxDwords);
     if (o <= kMaxTileStride) {
         const uint32_t S = static_cast<uint32_t>(o);
@@ -608,6 +772,25 @@ int srpc_plan_force_path(srpc_plan* p, int path) {
     return SRPC_E_UNSUPPORTED;
 }
 
+int srpc_plan_tune(srpc_plan* p, int knob, int value) {
+    if (!p) return SRPC_E_INVALID;
+    switch (knob) {
+    case SRPC_TUNE_RECORDS_PER_LANE:
+        if (value != 1 && value != 4) return SRPC_E_INVALID;
+        p->dv.rpl = value;
+        return SRPC_OK;
+    case SRPC_TUNE_ITER:
+        if (value != 1 && value != 2 && value != 4 && value != 8) return SRPC_E_INVALID;
+        p->dv.iter = value;
+        return SRPC_OK;
+    case SRPC_TUNE_NONTEMPORAL:
+        if (value < 0 || value > 3) return SRPC_E_INVALID;
+        p->dv.nt = value;
+        return SRPC_OK;
+    default: return SRPC_E_INVALID;
+    }
+}
+
 int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8_t* wire,
                   uint64_t wire_cap, void* stream) {
     if (!p) return SRPC_E_INVALID;
@@ -620,17 +803,10 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
     auto s = static_cast<hipStream_t>(stream);
     if (p->path == SRPC_PATH_DWORD) {
         const DwordMap m = make_dword_map(p, cols);
-        switch (p->stride / 4) {
-        case 1: return launch_dword_pack<1>(m, wire, n, s);
-        case 2: return launch_dword_pack<2>(m, wire, n, s);
-        case 3: return launch_dword_pack<3>(m, wire, n, s);
-        case 4: return launch_dword_pack<4>(m, wire, n, s);
-        case 5: return launch_dword_pack<5>(m, wire, n, s);
-        case 6: return launch_dword_pack<6>(m, wire, n, s);
-        case 7: return launch_dword_pack<7>(m, wire, n, s);
-        case 8: return launch_dword_pack<8>(m, wire, n, s);
-        default: return SRPC_E_UNSUPPORTED;
-        }
+        const bool x4 = p->dv.rpl == 4 && p->all4 && check_cols_aligned(cols, p->nfields, 16);
+        DwordVariant v = p->dv;
+        v.rpl = x4 ? 4 : 1;
+        return launch_dword_any(true, m, wire, n, static_cast<uint32_t>(p->stride / 4), v, s);
     }
     const TileArgs a = make_tile_args(p, cols);
     const uint64_t ntiles = (n + p->tile_R - 1) / p->tile_R;
@@ -666,17 +842,12 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     if (n_fit == 0) return ret;
     if (p->path == SRPC_PATH_DWORD) {
         const DwordMap m = make_dword_map(p, reinterpret_cast<const void* const*>(cols));
-        switch (p->stride / 4) {
-        case 1: rc = launch_dword_unpack<1>(m, wire, n_fit, s); break;
-        case 2: rc = launch_dword_unpack<2>(m, wire, n_fit, s); break;
-        case 3: rc = launch_dword_unpack<3>(m, wire, n_fit, s); break;
-        case 4: rc = launch_dword_unpack<4>(m, wire, n_fit, s); break;
-        case 5: rc = launch_dword_unpack<5>(m, wire, n_fit, s); break;
-        case 6: rc = launch_dword_unpack<6>(m, wire, n_fit, s); break;
-        case 7: rc = launch_dword_unpack<7>(m, wire, n_fit, s); break;
-        case 8: rc = launch_dword_unpack<8>(m, wire, n_fit, s); break;
-        default: rc = SRPC_E_UNSUPPORTED;
-        }
+        const bool x4 = p->dv.rpl == 4 && p->all4 &&
+                        check_cols_aligned(reinterpret_cast<const void* const*>(cols), p->nfields, 16);
+        DwordVariant v = p->dv;
+        v.rpl = x4 ? 4 : 1;
+        rc = launch_dword_any(false, m, const_cast<uint8_t*>(wire), n_fit,
+                              static_cast<uint32_t>(p->stride / 4), v, s);
         return rc ? rc : ret;
     }
     const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols));

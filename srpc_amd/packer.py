@@ -130,6 +130,14 @@ class GpuPacker:
     def force_path(self, path: int) -> None:
         check(_lib.lib().srpc_plan_force_path(self._h, path), "srpc_plan_force_path")
 
+    def tune(self, records_per_lane: int | None = None, iters: int | None = None,
+             nontemporal: int | None = None) -> None:
+        """DWORD-path performance knobs (srpc_plan_tune); output bytes never change."""
+        L = _lib.lib()
+        for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal)):
+            if val is not None:
+                check(L.srpc_plan_tune(self._h, knob, int(val)), "srpc_plan_tune")
+
     def wire_bytes(self, n: int) -> int:
         return n * self.record_bytes
 

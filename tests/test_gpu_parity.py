@@ -167,6 +167,26 @@ def test_random_schemas_vs_oracle(n, schema):
             assert a.tobytes() == b.tobytes()
 
 
+@pytest.mark.parametrize("schema", ["quad", "number", "two", "i64x2"])
+def test_dword_variants_identical(schema):
+    sch = {"quad": QUAD, "number": NUMBER, "two": TWO_NUMBERS,
+           "i64x2": Schema.of("L", ("x", "int64"), ("y", "int64"))}[schema]
+    kinds = sch.kinds
+    n = 3 * 4096 + 7  # exercises the x4 body and the 1-record tail
+    rng = np.random.default_rng(11)
+    cols = [rng.integers(0, 256, n * np.dtype(oracle.KIND_DTYPE[k]).itemsize, dtype=np.uint8)
+            .view(oracle.KIND_DTYPE[k]) for k in kinds]
+    want = oracle.pack(kinds, cols, n)
+    p = GpuPacker(sch)
+    for rpl in (1, 4):
+        for it in (1, 2, 4, 8):
+            for nt in range(4):
+                p.tune(rpl, it, nt)
+                assert gpu_pack(p, cols, n) == want, (rpl, it, nt)
+                rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+                assert rc == 0 and all(a.tobytes() == b.tobytes() for a, b in zip(cols, back)), (rpl, it, nt)
+
+
 # ---- envelopes (Calculator.square) ---------------------------------------------
 
 def test_square_request_envelope(golden_dir, manifest):
