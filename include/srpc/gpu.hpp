@@ -1,0 +1,181 @@
+// srpc/gpu.hpp -- batched GPU packing for sRPC messages (host C++ over the C ABI).
+//
+// srpc::gpu::batch_packer<T> packs / unpacks N records of a generated message
+// type T in one launch on an MI355X, producing exactly the bytes of
+//     srpc::packer p; for (auto& r : batch) p << r;                   (body)
+//     for (auto& r : batch) p.pack_request(request_t<T>{method, r});  (request)
+//     for (auto& r : batch) p.pack_response(response_t<T>{code, r});  (response)
+// The field list comes from T::fields at compile time (nested messages are
+// flattened, as pack_struct inlines them: reference packer.hpp:172-178,
+// 183-186), so no hand-written schema is needed.
+//
+// Records live on the device as one column per flattened field (SoA), the
+// wire bytes as one contiguous buffer.  All pointers are device pointers; the
+// stream is a hipStream_t passed as void*.  Link with -lsrpc_gpu
+// (srpc_amd/libsrpc_gpu.so).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "../srpc_gpu.h"
+#include "core.hpp"
+#include "packer.hpp"
+
+namespace srpc::gpu {
+
+template <typename T, typename M>
+using member_t = std::remove_cvref_t<decltype(std::declval<T const&>().*std::declval<M>())>;
+
+/// srpc_kind of one C++ field type (the IDL table, parser.hpp:253-290).
+template <typename F>
+constexpr int32_t kind_of() {
+    if constexpr (std::is_same_v<F, bool>) return SRPC_KIND_BOOL;
+    else if constexpr (std::is_same_v<F, char>) return SRPC_KIND_CHAR;
+    else if constexpr (std::is_same_v<F, std::string>) return SRPC_KIND_STRING;
+    else if constexpr (std::is_integral_v<F> || std::is_enum_v<F>) {
+        static_assert(sizeof(F) == 1 || sizeof(F) == 2 || sizeof(F) == 4 || sizeof(F) == 8);
+        if constexpr (sizeof(F) == 1) return SRPC_KIND_INT8;
+        else if constexpr (sizeof(F) == 2) return SRPC_KIND_INT16;
+        else if constexpr (sizeof(F) == 4) return SRPC_KIND_INT32;
+        else return SRPC_KIND_INT64;
+    } else {
+        static_assert(sizeof(F) == 0, "srpc::gpu: unsupported field type");
+        return 0;
+    }
+}
+
+/// Visit every leaf field of T (nested messages flattened) in wire order:
+/// fn(const Leaf& value_in_record) for a const record, or with a mutable one.
+template <typename T, typename Rec, typename Fn>
+void for_each_leaf(Rec& rec, Fn&& fn) {
+    std::apply(
+        [&](const auto&... m) {
+            (
+                [&] {
+                    auto& v = rec.*(std::get<MEMBER_ADDR>(m));
+                    using F = std::remove_cvref_t<decltype(v)>;
+                    if constexpr (std::is_base_of_v<message_base, F>) for_each_leaf<F>(v, fn);
+                    else fn(v);
+                }(),
+                ...);
+        },
+        T::fields);
+}
+
+template <SrpcMessage T>
+std::vector<int32_t> flat_kinds() {
+    std::vector<int32_t> k;
+    T probe{};
+    for_each_leaf<T>(probe, [&](const auto& v) { k.push_back(kind_of<std::remove_cvref_t<decltype(v)>>()); });
+    return k;
+}
+
+/// The constant header that pack_request / pack_response emit before a body
+/// of T -- produced by the scalar packer itself, so the bytes cannot differ.
+template <SrpcMessage T>
+std::vector<uint8_t> request_prefix(std::string const& method) {
+    packer p;
+    p << method << T::name;
+    return std::vector<uint8_t>(p.data(), p.data() + p.size());
+}
+
+template <SrpcMessage T>
+std::vector<uint8_t> response_prefix(rpc_status_code code) {
+    packer p;
+    p << code << T::name;
+    return std::vector<uint8_t>(p.data(), p.data() + p.size());
+}
+
+/// Host-side SoA image of a batch: one byte column per flattened fixed field.
+template <SrpcMessage T>
+struct host_columns {
+    std::vector<std::vector<uint8_t>> col;
+    uint64_t n = 0;
+
+    void scatter(std::vector<T> const& recs) {
+        n = recs.size();
+        col.clear();
+        T probe{};
+        for_each_leaf<T>(probe, [&](const auto& v) { col.emplace_back(n * sizeof(v)); });
+        for (uint64_t i = 0; i < n; ++i) {
+            size_t f = 0;
+            for_each_leaf<T>(recs[i], [&](const auto& v) {
+                std::memcpy(col[f++].data() + i * sizeof(v), &v, sizeof(v));
+            });
+        }
+    }
+
+    void gather(std::vector<T>& recs) const {
+        recs.resize(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            size_t f = 0;
+            for_each_leaf<T>(recs[i], [&](auto& v) {
+                std::memcpy(&v, col[f++].data() + i * sizeof(v), sizeof(v));
+            });
+        }
+    }
+};
+
+class plan_error : public std::runtime_error {
+public:
+    plan_error(const char* what, int code)
+        : std::runtime_error(std::string(what) + ": " + srpc_status_string(code)), code(code) {}
+    int code;
+};
+
+/// One plan per (message type, envelope, device).
+template <SrpcMessage T>
+class batch_packer {
+public:
+    explicit batch_packer(int device = 0) : batch_packer(std::vector<uint8_t>{}, device) {}
+
+    static batch_packer request(std::string const& method, int device = 0) {
+        return batch_packer(request_prefix<T>(method), device);
+    }
+    static batch_packer response(rpc_status_code code = RPC_SUCCESS, int device = 0) {
+        return batch_packer(response_prefix<T>(code), device);
+    }
+
+    batch_packer(batch_packer&& o) noexcept : _plan(o._plan), _nfields(o._nfields), _rb(o._rb) { o._plan = nullptr; }
+    batch_packer(batch_packer const&) = delete;
+    batch_packer& operator=(batch_packer const&) = delete;
+    ~batch_packer() {
+        if (_plan) srpc_plan_destroy(_plan);
+    }
+
+    uint64_t record_bytes() const { return _rb; }
+    uint32_t nfields() const { return _nfields; }
+    srpc_plan* plan() const { return _plan; }
+
+    /// d_cols: nfields() device column pointers.  Returns an srpc status.
+    int pack(const void* const* d_cols, uint64_t n, uint8_t* d_wire, uint64_t wire_cap,
+             void* stream = nullptr) const {
+        return srpc_gpu_pack(_plan, d_cols, n, d_wire, wire_cap, stream);
+    }
+    int unpack(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, void* const* d_cols,
+               srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
+        return srpc_gpu_unpack(_plan, d_wire, wire_len, n, d_cols, d_status, stream);
+    }
+
+private:
+    batch_packer(std::vector<uint8_t> const& prefix, int device) {
+        const std::vector<int32_t> kinds = flat_kinds<T>();
+        srpc_schema_desc d{static_cast<uint32_t>(kinds.size()), kinds.data(), prefix.empty() ? nullptr : prefix.data(),
+                           static_cast<uint32_t>(prefix.size())};
+        if (int rc = srpc_plan_create(&d, device, &_plan); rc != SRPC_OK) throw plan_error("srpc_plan_create", rc);
+        _nfields = static_cast<uint32_t>(kinds.size());
+        srpc_plan_record_bytes(_plan, &_rb);
+    }
+
+    srpc_plan* _plan = nullptr;
+    uint32_t _nfields = 0;
+    uint64_t _rb = 0;
+};
+
+}  // namespace srpc::gpu

@@ -1,0 +1,337 @@
+// C++ API mirror test: the reference's packer and server tests, restated
+// against this repository's headers (include/srpc/*.hpp).
+//   - the 12 sections of the reference tests/packer_test.cpp (:91-436)
+//   - the in-process dispatch of tests/server_test.cpp:113-139 (5 -> 25)
+//   - the loopback socket round trip the reference left commented out
+//     (server_test.cpp:149-165), here over 127.0.0.1 with several calls on
+//     one channel
+//   - bounds behaviour of the hardened reads
+#include <srpc/core.hpp>
+#include <srpc/packer.hpp>
+#include <srpc/server.hpp>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <limits>
+#include <string>
+#include <thread>
+#include <vector>
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond)                                                              \
+    do {                                                                         \
+        if (cond) {                                                              \
+            ++g_pass;                                                            \
+        } else {                                                                 \
+            ++g_fail;                                                            \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+        }                                                                        \
+    } while (0)
+
+namespace srpc {
+
+struct single_primitive : public message_base {
+    int8_t arg1;
+    static constexpr const char* name = "single_primitive";
+    static constexpr auto fields = std::make_tuple(STRUCT_MEMBER(single_primitive, arg1, "single_primitive::arg1"));
+    bool operator==(const single_primitive& o) const noexcept { return arg1 == o.arg1; }
+    void unpack(buffer::ptr bp) override {
+        packer p(bp);
+        p >> arg1;
+    }
+};
+
+struct multiple_primitives : public message_base {
+    int8_t arg1;
+    char arg2;
+    int64_t arg3;
+    std::string arg4;
+    static constexpr const char* name = "multiple_primitives";
+    static constexpr auto fields = std::make_tuple(
+        STRUCT_MEMBER(multiple_primitives, arg1, "multiple_primitives::arg1"),
+        STRUCT_MEMBER(multiple_primitives, arg2, "multiple_primitives::arg2"),
+        STRUCT_MEMBER(multiple_primitives, arg3, "multiple_primitives::arg3"),
+        STRUCT_MEMBER(multiple_primitives, arg4, "multiple_primitives::arg4"));
+    bool operator==(const multiple_primitives& o) const noexcept {
+        return arg1 == o.arg1 && arg2 == o.arg2 && arg3 == o.arg3 && arg4 == o.arg4;
+    }
+    void unpack(buffer::ptr bp) override {
+        packer p(bp);
+        p >> arg1;
+        p >> arg2;
+        p >> arg3;
+        p >> arg4;
+    }
+};
+
+struct nested_message : public message_base {
+    int64_t arg1;
+    single_primitive arg2;
+    multiple_primitives arg3;
+    static constexpr const char* name = "nested_message";
+    static constexpr auto fields = std::make_tuple(STRUCT_MEMBER(nested_message, arg1, "nested_message::arg1"),
+                                                   STRUCT_MEMBER(nested_message, arg2, "nested_message::arg2"),
+                                                   STRUCT_MEMBER(nested_message, arg3, "nested_message::arg3"));
+    bool operator==(const nested_message& o) const noexcept {
+        return arg1 == o.arg1 && arg2 == o.arg2 && arg3 == o.arg3;
+    }
+    void unpack(buffer::ptr bp) override {
+        packer p(bp);
+        p >> arg1;
+        single_primitive a2;
+        a2.unpack(bp);
+        arg2 = std::move(a2);
+        multiple_primitives a3;
+        a3.unpack(bp);
+        arg3 = std::move(a3);
+    }
+};
+
+}  // namespace srpc
+
+using namespace srpc;
+
+static std::vector<uint8_t> str(const std::string& s) {
+    std::vector<uint8_t> v(8 + s.size());
+    uint64_t n = s.size();
+    std::memcpy(v.data(), &n, 8);
+    std::memcpy(v.data() + 8, s.data(), s.size());
+    return v;
+}
+static std::vector<uint8_t> cat(std::initializer_list<std::vector<uint8_t>> parts) {
+    std::vector<uint8_t> o;
+    for (auto& p : parts) o.insert(o.end(), p.begin(), p.end());
+    return o;
+}
+static const std::vector<uint8_t> SP_BODY{5};
+static const std::vector<uint8_t> MP_BODY = cat({{22, 'z', 255, 255, 255, 255, 255, 255, 255, 127}, str("testing_string")});
+static const std::vector<uint8_t> NM_BODY = cat({{255, 255, 255, 255, 255, 255, 255, 127}, SP_BODY, MP_BODY});
+
+static single_primitive make_sp() {
+    single_primitive sp;
+    sp.arg1 = 5;
+    return sp;
+}
+static multiple_primitives make_mp() {
+    multiple_primitives mp;
+    mp.arg1 = 22;
+    mp.arg2 = 'z';
+    mp.arg3 = std::numeric_limits<int64_t>::max();
+    mp.arg4 = "testing_string";
+    return mp;
+}
+static nested_message make_nm() {
+    nested_message nm;
+    nm.arg1 = std::numeric_limits<int64_t>::max();
+    nm.arg2 = make_sp();
+    nm.arg3 = make_mp();
+    return nm;
+}
+
+template <typename T>
+static std::vector<uint8_t> packed_request(T v, const char* method) {
+    packer pr;
+    request_t<T> req;
+    req.set_value(std::move(v));
+    req.set_method_name(method);
+    pr.pack_request(req);
+    return *pr.buf();
+}
+
+template <typename T>
+static std::vector<uint8_t> packed_response(T v, rpc_status_code c) {
+    packer pr;
+    response_t<T> res;
+    res.set_value(std::move(v));
+    res.set_code(c);
+    pr.pack_response(res);
+    return *pr.buf();
+}
+
+static void register_test_messages() {
+    message_registry["single_primitive"] = []() -> std::unique_ptr<single_primitive> {
+        return std::make_unique<single_primitive>();
+    };
+    message_registry["multiple_primitives"] = []() -> std::unique_ptr<multiple_primitives> {
+        return std::make_unique<multiple_primitives>();
+    };
+    message_registry["nested_message"] = []() -> std::unique_ptr<nested_message> {
+        return std::make_unique<nested_message>();
+    };
+}
+
+static void test_pack_requests_and_responses() {
+    // packer_test.cpp:91-178
+    CHECK(packed_request(make_sp(), "test") == cat({str("test"), str("single_primitive"), SP_BODY}));
+    CHECK(packed_request(make_mp(), "test") == cat({str("test"), str("multiple_primitives"), MP_BODY}));
+    CHECK(packed_request(make_nm(), "test") == cat({str("test"), str("nested_message"), NM_BODY}));
+    // packer_test.cpp:180-264
+    CHECK(packed_response(make_sp(), RPC_SUCCESS) == cat({{0}, str("single_primitive"), SP_BODY}));
+    CHECK(packed_response(make_mp(), RPC_ERR_RECV_TIMEOUT) == cat({{2}, str("multiple_primitives"), MP_BODY}));
+    CHECK(packed_response(make_nm(), RPC_ERR_FUNCTION_NOT_REGISTERED) ==
+          cat({{1}, str("nested_message"), NM_BODY}));
+    // the first bytes exactly as written in packer_test.cpp:102-107
+    std::vector<uint8_t> lit{4, 0, 0, 0, 0, 0, 0, 0, 't', 'e', 's', 't', 16, 0, 0, 0, 0, 0, 0, 0,
+                             's', 'i', 'n', 'g', 'l', 'e', '_', 'p', 'r', 'i', 'm', 'i', 't', 'i', 'v', 'e', 5};
+    CHECK(packed_request(make_sp(), "test") == lit);
+}
+
+static void test_unpack_requests_and_responses() {
+    register_test_messages();
+    {  // packer_test.cpp:277-292
+        packer pr(cat({str("test"), str("single_primitive"), SP_BODY}));
+        auto r = pr.unpack_request<single_primitive>();
+        CHECK(r.value() == make_sp());
+        CHECK(r.method_name() == "test");
+    }
+    {  // :294-316 (method "test_method")
+        packer pr(cat({str("test_method"), str("multiple_primitives"), MP_BODY}));
+        auto r = pr.unpack_request<multiple_primitives>();
+        CHECK(r.value() == make_mp());
+        CHECK(r.method_name() == "test_method");
+    }
+    {  // :318-351
+        packer pr(cat({str("test"), str("nested_message"), NM_BODY}));
+        auto r = pr.unpack_request<nested_message>();
+        CHECK(r.value() == make_nm());
+        CHECK(r.method_name() == "test");
+        CHECK(pr.size() == 0 && pr.ok());
+    }
+    {  // :365-379
+        packer pr(cat({{0}, str("single_primitive"), SP_BODY}));
+        auto r = pr.unpack_response<single_primitive>();
+        CHECK(r.value() == make_sp());
+        CHECK(r.code() == RPC_SUCCESS);
+    }
+    {  // :381-402
+        packer pr(cat({{2}, str("multiple_primitives"), MP_BODY}));
+        auto r = pr.unpack_response<multiple_primitives>();
+        CHECK(r.value() == make_mp());
+        CHECK(r.code() == RPC_ERR_RECV_TIMEOUT);
+    }
+    {  // :404-435
+        packer pr(cat({{1}, str("nested_message"), NM_BODY}));
+        auto r = pr.unpack_response<nested_message>();
+        CHECK(r.value() == make_nm());
+        CHECK(r.code() == RPC_ERR_FUNCTION_NOT_REGISTERED);
+    }
+}
+
+static void test_bodies_and_bounds() {
+    packer p;
+    p << make_mp() << make_sp() << int16_t(-2) << true << std::string("ab");
+    CHECK(*p.buf() == cat({MP_BODY, SP_BODY, {0xfe, 0xff, 1}, str("ab")}));
+    // truncated string length: hardened read flags instead of terminating
+    std::vector<uint8_t> bad = cat({{22, 'z', 255, 255, 255, 255, 255, 255, 255, 127}, {100, 0, 0, 0, 0, 0, 0, 0, 'x'}});
+    auto bp = std::make_shared<buffer>(bad);
+    multiple_primitives mp;
+    mp.unpack(bp);
+    CHECK(bp->failed());
+    CHECK(mp.arg1 == 22 && mp.arg3 == std::numeric_limits<int64_t>::max() && mp.arg4.empty());
+    // short fixed field
+    packer q(std::vector<uint8_t>{1, 2, 3});
+    int32_t v = 7;
+    q >> v;
+    CHECK(!q.ok() && v == 0);
+}
+
+// ---- server ------------------------------------------------------------------
+
+struct number : public message_base {
+    int64_t num;
+    static constexpr const char* name = "number";
+    static constexpr auto fields = std::make_tuple(STRUCT_MEMBER(number, num, "number::num"));
+    void unpack(buffer::ptr bp) override {
+        packer p(bp);
+        p >> num;
+    }
+    bool operator==(const number& o) const noexcept { return o.num == num; }
+};
+
+struct calculate_servicer : servicer_base {
+    virtual number square(number&) { throw std::runtime_error("Method not implemented!"); }
+    static constexpr const char* name = "calculate";
+    static constexpr auto methods = std::make_tuple(STRUCT_MEMBER(calculate_servicer, square, "calculate_servicer::square"));
+};
+
+struct calculator : public calculate_servicer {
+    number square(number& req) override {
+        number out;
+        out.num = req.num * req.num;
+        return out;
+    }
+};
+
+static void test_server_dispatch() {
+    // server_test.cpp:113-139
+    message_registry["number"] = []() -> std::unique_ptr<number> { return std::make_unique<number>(); };
+    server s;
+    calculator c;
+    number input;
+    input.num = 5;
+    request_t<number> req;
+    req.set_value(std::move(input));
+    req.set_method_name("calculate_servicer::square");
+    packer::ptr p = std::make_shared<packer>();
+    p->pack_request(req);
+    std::string funcname;
+    (*p) >> funcname;
+    s.register_service(c);
+    packer::ptr rp = s.call(funcname, p);
+    response_t<number> response = rp->unpack_response<number>();
+    CHECK(response.code() == RPC_SUCCESS);
+    CHECK(response.value().num == 25);
+    // unknown function: one status byte, no crash
+    packer::ptr p2 = std::make_shared<packer>();
+    packer::ptr r2 = s.call("nope", p2);
+    CHECK(*r2->buf() == std::vector<uint8_t>{RPC_ERR_FUNCTION_NOT_REGISTERED});
+}
+
+static void test_loopback_socket() {
+    const std::string port = "18081";
+    calculator c;
+    server s;
+    s.register_service(c);
+    std::thread th([&] {
+        int lfd = transport::create_server_socket(port);
+        sockaddr_storage a{};
+        socklen_t al = sizeof(a);
+        int fd = accept(lfd, reinterpret_cast<sockaddr*>(&a), &al);
+        s.serve_connection(fd);
+        close(fd);
+        close(lfd);
+    });
+    int fd = -1;
+    for (int i = 0; i < 100 && fd < 0; ++i) {
+        fd = transport::create_client_socket("127.0.0.1", port);
+        if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    CHECK(fd >= 0);
+    for (int64_t x : {5, -7, 46340}) {  // several calls on one channel
+        packer pr;
+        request_t<number> req;
+        number n;
+        n.num = x;
+        req.set_value(std::move(n));
+        req.set_method_name("calculate_servicer::square");
+        pr.pack_request(req);
+        transport::send_data(fd, (*pr.buf()).data(), pr.size());
+        message_t res = transport::recv_data(fd);
+        packer rpr(res.data(), res.size());
+        auto msg = rpr.unpack_response<number>();
+        CHECK(msg.code() == RPC_SUCCESS && msg.value().num == x * x);
+    }
+    close(fd);
+    th.join();
+}
+
+int main() {
+    test_pack_requests_and_responses();
+    test_unpack_requests_and_responses();
+    test_bodies_and_bounds();
+    test_server_dispatch();
+    test_loopback_socket();
+    std::printf("packer_test: %d passed, %d failed\n", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}
