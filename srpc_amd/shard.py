@@ -40,6 +40,11 @@ def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None):
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host memory only: stage through the CPU (test rehearsals;
+        # production runs use RCCL, which reads and writes HBM directly)
+        out = gather_packed(local.cpu(), record_bytes, n, root, group)
+        return out.to(local.device) if out is not None else None
     ranges = shard_ranges(n, world)
     sizes = [(hi - lo) * record_bytes for lo, hi in ranges]
     if local.numel() != sizes[rank]:
