@@ -141,17 +141,39 @@ int srpc_gpu_unpack(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_
                     uint64_t n, void* const* d_cols, srpc_unpack_status* d_status,
                     void* stream);
 
-/* ---- variable-length (string) schemas -------------------------------------
- * String field f is given as chars d_cols[f] plus n+1 u64 byte offsets
- * d_str_offs[f] (offsets[0] may be nonzero; lengths are offs[i+1]-offs[i]).
- * Pack writes the record start offsets (n+1 values, [0] = 0, [n] = total
- * bytes) to d_rec_offs and needs `scratch_bytes` of device scratch from
- * srpc_plan_var_scratch_bytes. */
+/* ---- variable-length (string) schemas (SRPC_PATH_VAR) ----------------------
+ * A string field f is given as its chars d_cols[f] plus n+1 u64 byte offsets
+ * d_str_offs[f] (lengths are offs[i+1]-offs[i]; offs[0] need not be 0).
+ * d_str_offs is a host array of nfields device pointers, NULL for fixed fields.
+ * Record starts: d_rec_offs, n+1 u64, [0] = 0, [n] = total wire bytes.
+ * Both calls need `scratch_bytes` of device scratch (8-byte aligned) from
+ * srpc_plan_var_scratch_bytes; like the fixed calls they are stream-ordered
+ * and allocate nothing. */
 int srpc_plan_var_scratch_bytes(const srpc_plan* plan, uint64_t n, uint64_t* out);
+
+/* Pack n records (reference: the `p << r` / pack_request loop over records
+ * with std::string members, packer.hpp:193-198).  Writes d_rec_offs[0..n]
+ * (an exclusive scan of the record sizes) and the wire bytes.  If the batch
+ * needs more than wire_cap bytes, only the first wire_cap are written and
+ * *d_status (if non-NULL) gets SRPC_STATUS_BOUNDS with the first record that
+ * did not fit; the caller reads d_rec_offs[n] for the size actually needed. */
 int srpc_gpu_pack_var(const srpc_plan* plan, const void* const* d_cols,
                       const uint64_t* const* d_str_offs, uint64_t n, uint8_t* d_wire,
-                      uint64_t wire_cap, uint64_t* d_rec_offs, void* d_scratch,
-                      uint64_t scratch_bytes, void* stream);
+                      uint64_t wire_cap, uint64_t* d_rec_offs, srpc_unpack_status* d_status,
+                      void* d_scratch, uint64_t scratch_bytes, void* stream);
+
+/* Unpack n records whose starts are d_rec_offs[0..n] (the record index the
+ * packer produced, or the frame boundaries of a socket stream) (reference:
+ * pipe_output<std::string>, packer.hpp:216-222).  Fixed fields go to
+ * d_cols[f] (aligned to their size); string field f's bytes go back to back
+ * into d_cols[f] (16-byte aligned, room for wire_len bytes) with offsets
+ * d_str_offs[f][0..n].  Prefix mismatches, string lengths past a record's
+ * end and records whose size disagrees with the index are reported in
+ * *d_status. */
+int srpc_gpu_unpack_var(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len,
+                        uint64_t n, const uint64_t* d_rec_offs, void* const* d_cols,
+                        uint64_t* const* d_str_offs, srpc_unpack_status* d_status,
+                        void* d_scratch, uint64_t scratch_bytes, void* stream);
 
 /* ---- utilities --------------------------------------------------------------*/
 

@@ -1,0 +1,103 @@
+// plan.h -- internal: the srpc_plan object and helpers shared by the kernel
+// translation units of libsrpc_gpu.so (srpc_gpu.hip: fixed-size records,
+// var.hip: records with string fields).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "srpc_gpu.h"
+
+namespace srpc_impl {
+
+constexpr int kBlock = 256;          // 4 waves of 64
+constexpr int kMaxFields = 32;
+constexpr int kMaxDwords = 8;        // DWORD path: records of up to 32 bytes
+constexpr uint32_t kTileTarget = 8192;   // TILE path: ~8 KiB LDS image per tile
+constexpr uint32_t kMaxTileStride = 2048;
+constexpr uint32_t kMaxPrefix = 1024;
+
+// Variant bits (srpc_plan_tune SRPC_TUNE_NT): non-temporal stores / loads.
+constexpr int kNtStore = 1;
+constexpr int kNtLoad = 2;
+
+// DWORD-path variant: records per lane (1 or 4), iterations per lane, NT bits.
+// Default = the fastest in the steady-state bench loop on MI355X (16M Quad,
+// profiles/r01_tune.log): one record per lane, one iteration, non-temporal
+// loads and stores (streamed bytes are touched once per kernel).
+struct DwordVariant {
+    int rpl = 1;
+    int iter = 1;
+    int nt = kNtStore | kNtLoad;
+};
+
+__device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag, uint64_t rec) {
+    atomicOr(&st->flags, flag);
+    atomicMin(reinterpret_cast<unsigned long long*>(&st->first_bad_record),
+              static_cast<unsigned long long>(rec));
+}
+
+inline int kind_size(int32_t k) {
+    switch (k) {
+    case SRPC_KIND_BOOL:
+    case SRPC_KIND_INT8:
+    case SRPC_KIND_CHAR: return 1;
+    case SRPC_KIND_INT16: return 2;
+    case SRPC_KIND_INT32: return 4;
+    case SRPC_KIND_INT64: return 8;
+    case SRPC_KIND_STRING: return 0;
+    default: return -1;
+    }
+}
+
+inline uint32_t gcd_u32(uint32_t a, uint32_t b) {
+    while (b) {
+        uint32_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+inline uint32_t ilog2(uint32_t s) { return s == 1 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3; }
+
+inline bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace srpc_impl
+
+// The object behind the opaque srpc_plan* of include/srpc_gpu.h.
+struct srpc_plan {
+    int device = 0;
+    uint32_t nfields = 0;
+    int32_t kinds[srpc_impl::kMaxFields] = {};
+    uint32_t size[srpc_impl::kMaxFields] = {};
+    uint32_t off[srpc_impl::kMaxFields] = {};   // offset within record, prefix included
+    uint32_t prefix_len = 0;
+    uint8_t h_prefix[srpc_impl::kMaxPrefix] = {};
+    uint8_t* d_prefix = nullptr;
+    uint64_t stride = 0;             // fixed record bytes (0 for string schemas)
+    bool has_string = false;
+    bool dword_ok = false;
+    int path = 0;
+    uint32_t tile_R = 0, tile_L = 0;
+    int tile_grid = 0;               // resident workgroups for grid-stride tiles
+    size_t tile_lds = 0;
+    bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
+    srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
+    // string schemas (SRPC_PATH_VAR)
+    uint32_t nstrings = 0;
+    uint32_t fixed_bytes = 0;        // prefix + fixed fields + 8 per string field
+};

@@ -29,16 +29,12 @@
 #include <cstring>
 #include <new>
 
+#include "plan.h"
 #include "srpc_gpu.h"
 
 namespace {
+using namespace srpc_impl;
 
-constexpr int kBlock = 256;          // 4 waves of 64
-constexpr int kMaxFields = 32;
-constexpr int kMaxDwords = 8;        // DWORD path: records of up to 32 bytes
-constexpr uint32_t kTileTarget = 8192;   // TILE path: ~8 KiB LDS image per tile
-constexpr uint32_t kMaxTileStride = 2048;
-constexpr uint32_t kMaxPrefix = 1024;
 
 // ---------------------------------------------------------------------------
 // Kernel argument blocks (all wave-uniform: they live in SGPRs / kernarg).
@@ -66,11 +62,6 @@ struct TileArgs {
     uint32_t L;                      // template period lcm(stride, 16), divides R*stride
 };
 
-__device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag, uint64_t rec) {
-    atomicOr(&st->flags, flag);
-    atomicMin(reinterpret_cast<unsigned long long*>(&st->first_bad_record),
-              static_cast<unsigned long long>(rec));
-}
 
 // ---------------------------------------------------------------------------
 // DWORD path
@@ -78,19 +69,6 @@ __device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Variant bits (srpc_plan_tune SRPC_TUNE_NT): non-temporal stores / loads.
-constexpr int kNtStore = 1;
-constexpr int kNtLoad = 2;
-
-// DWORD-path variant: records per lane (1 or 4), iterations per lane, NT bits.
-// Default = the fastest in the steady-state bench loop on MI355X (16M Quad,
-// profiles/r01_tune.log): one record per lane, one iteration, non-temporal
-// loads and stores (streamed bytes are touched once per kernel).
-struct DwordVariant {
-    int rpl = 1;
-    int iter = 1;
-    int nt = kNtStore | kNtLoad;
-};
 
 template <int NT, typename T>
 __device__ __forceinline__ T ld(const T* p) {
@@ -462,65 +440,9 @@ __global__ __launch_bounds__(kBlock) void k_fill_splitmix(FillArgs a, uint32_t n
 // ===========================================================================
 // Host side: plans and the C ABI
 // ===========================================================================
-struct srpc_plan {
-    int device = 0;
-    uint32_t nfields = 0;
-    int32_t kinds[kMaxFields] = {};
-    uint32_t size[kMaxFields] = {};
-    uint32_t off[kMaxFields] = {};   // offset within record, prefix included
-    uint32_t prefix_len = 0;
-    uint8_t h_prefix[kMaxPrefix] = {};
-    uint8_t* d_prefix = nullptr;
-    uint64_t stride = 0;             // fixed record bytes (0 for string schemas)
-    bool has_string = false;
-    bool dword_ok = false;
-    int path = 0;
-    uint32_t tile_R = 0, tile_L = 0;
-    int tile_grid = 0;               // resident workgroups for grid-stride tiles
-    size_t tile_lds = 0;
-    bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
-    DwordVariant dv;                 // DWORD-path variant (srpc_plan_tune)
-};
 
 namespace {
-
-int kind_size(int32_t k) {
-    switch (k) {
-    case SRPC_KIND_BOOL:
-    case SRPC_KIND_INT8:
-    case SRPC_KIND_CHAR: return 1;
-    case SRPC_KIND_INT16: return 2;
-    case SRPC_KIND_INT32: return 4;
-    case SRPC_KIND_INT64: return 8;
-    case SRPC_KIND_STRING: return 0;
-    default: return -1;
-    }
-}
-
-uint32_t gcd_u32(uint32_t a, uint32_t b) {
-    while (b) {
-        uint32_t t = a % b;
-        a = b;
-        b = t;
-    }
-    return a;
-}
-
-uint32_t ilog2(uint32_t s) { return s == 1 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3; }
-
-bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
+using namespace srpc_impl;
 
 template <int W, int ITER, int NT>
 int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, hipStream_t s) {
@@ -695,9 +617,21 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         o += static_cast<uint64_t>(s);
     }
     if (p->has_string) {
-        // Variable-length records are not in this build yet.
-        delete p;
-        return SRPC_E_UNSUPPORTED;
+        p->path = SRPC_PATH_VAR;
+        for (uint32_t f = 0; f < d->nfields; ++f) p->nstrings += p->size[f] == 0;
+        p->fixed_bytes = static_cast<uint32_t>(o + 8ull * p->nstrings);
+        p->stride = 0;
+        DeviceGuard g(device);
+        if (p->prefix_len) {
+            if (hipMalloc(&p->d_prefix, p->prefix_len) != hipSuccess ||
+                hipMemcpy(p->d_prefix, p->h_prefix, p->prefix_len, hipMemcpyHostToDevice) != hipSuccess) {
+                if (p->d_prefix) (void)hipFree(p->d_prefix);
+                delete p;
+                return SRPC_E_HIP;
+            }
+        }
+        *out = p;
+        return SRPC_OK;
     }
     p->stride = o;
     p->all4 = all4_fields;
@@ -793,7 +727,7 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
 
 int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8_t* wire,
                   uint64_t wire_cap, void* stream) {
-    if (!p) return SRPC_E_INVALID;
+    if (!p || p->has_string) return SRPC_E_INVALID;  // string schemas: srpc_gpu_pack_var
     if (n == 0) return SRPC_OK;
     if (!wire) return SRPC_E_INVALID;
     if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
@@ -817,7 +751,7 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
 
 int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
                     void* const* cols, srpc_unpack_status* st, void* stream) {
-    if (!p) return SRPC_E_INVALID;
+    if (!p || p->has_string) return SRPC_E_INVALID;  // string schemas: srpc_gpu_unpack_var
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
         hipLaunchKernelGGL(k_set_status, dim3(1), dim3(64), 0, s, st, 0u, 0ull);
@@ -856,20 +790,6 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     hipLaunchKernelGGL(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     return ret;
-}
-
-int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t* out) {
-    (void)n;
-    if (!p || !out) return SRPC_E_INVALID;
-    return SRPC_E_UNSUPPORTED;
-}
-
-int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_t* const* str_offs,
-                      uint64_t n, uint8_t* wire, uint64_t wire_cap, uint64_t* rec_offs, void* scratch,
-                      uint64_t scratch_bytes, void* stream) {
-    (void)p; (void)cols; (void)str_offs; (void)n; (void)wire; (void)wire_cap; (void)rec_offs;
-    (void)scratch; (void)scratch_bytes; (void)stream;
-    return SRPC_E_UNSUPPORTED;
 }
 
 int srpc_gpu_fill_splitmix_i32(int32_t* const* cols, uint32_t nfields, uint64_t n, uint64_t seed,

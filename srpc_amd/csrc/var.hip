@@ -1,0 +1,535 @@
+// var.hip -- records with string fields (SRPC_PATH_VAR).
+//
+// Wire format (reference include/srpc/packer.hpp): a string is a u64 LE length
+// followed by its bytes (pack_arg<std::string> 193-198, pipe_output<std::string>
+// 216-222); records are still back to back, so record i starts at the
+// exclusive prefix sum of the record sizes before it.
+//
+// PACK  (srpc_gpu_pack_var)
+//   1. k_scan_reduce / k_scan_partials / k_scan_apply: reduce-then-scan of the
+//      record sizes  size(i) = fixed_bytes + sum_f len(i, f)  into
+//      rec_offs[0..n] (u64).  Inside a workgroup: per-thread serial scan of 8
+//      items, a 64-lane wavefront scan of the thread totals (__shfl_up), and
+//      an LDS scan of the 4 wave totals.
+//   2. k_pack_var: the wire is cut into 4 KiB tiles; a tile's first record is
+//      found by a binary search of rec_offs, the next record starts are staged
+//      in LDS, and every lane builds one 16-byte chunk of output: it walks the
+//      records/segments (prefix, fixed fields, string length, string bytes)
+//      covering its 16 bytes, assembles them in an LDS staging slot and
+//      writes them with one 16-byte store.
+// UNPACK (srpc_gpu_unpack_var) -- needs the record start index rec_offs
+//   (produced by pack, or by frame lengths on a socket):
+//   1. k_unpack_var_walk: one record per lane: prefix check, string lengths
+//      and chars positions, record-size consistency (status word on error).
+//   2. scans of each string field's lengths -> str_offs[f][0..n].
+//   3. k_unpack_var_fixed: fixed fields to their columns.
+//   4. k_unpack_var_chars: output-chunk-centric copy of string bytes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+
+#include "plan.h"
+#include "srpc_gpu.h"
+
+namespace srpc_impl {
+namespace {
+
+constexpr int kScanItems = 8;
+constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 2048 items
+constexpr uint32_t kTileBytes = kBlock * 16;                                  // 4 KiB output tile
+constexpr uint32_t kWindow = 1024;  // record starts staged in LDS per tile
+constexpr int kVarGrid = 2048;      // resident workgroups for grid-stride tiles
+
+struct VarArgs {
+    const uint8_t* col[kMaxFields];   // fixed: column; string: chars
+    const uint64_t* soff[kMaxFields]; // string: n+1 char offsets
+    uint32_t size[kMaxFields];        // fixed size in bytes, 0 = string
+    uint32_t sidx[kMaxFields];        // string ordinal of a string field
+    const uint8_t* prefix;            // device copy of the constant header
+    uint32_t nfields, nstrings, prefix_len, fixed_bytes;
+};
+
+// ---- scans ------------------------------------------------------------------
+struct PackSizes {
+    VarArgs a;
+    __device__ uint64_t operator()(uint64_t i) const {
+        uint64_t s = a.fixed_bytes;
+        for (uint32_t f = 0; f < a.nfields; ++f)
+            if (a.size[f] == 0) s += a.soff[f][i + 1] - a.soff[f][i];
+        return s;
+    }
+};
+
+struct ArrayVals {
+    const uint64_t* v;
+    __device__ uint64_t operator()(uint64_t i) const { return v[i]; }
+};
+
+__device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// Exclusive scan of one value per thread over the workgroup; returns the
+// thread's exclusive prefix and writes the block total to *total.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* total) {
+    __shared__ uint64_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t inc = wave_inclusive_scan(x);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        before += (w < wave) ? wsum[w] : 0;
+        all += wsum[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - x;
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_t* partial) {
+    const uint64_t base = blockIdx.x * kScanBlock;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        const uint64_t i = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+        if (i < n) s += f(i);
+    }
+    uint64_t tot;
+    (void)block_exclusive_scan(s, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// One workgroup: exclusive scan of nb partials in place, partial[nb] = total.
+__global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uint64_t nb) {
+    const uint64_t per = (nb + kBlock - 1) / kBlock;
+    const uint64_t lo = threadIdx.x * per, hi = min(nb, lo + per);
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += partial[i];
+    uint64_t tot;
+    uint64_t run = block_exclusive_scan(s, &tot);
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint64_t v = partial[i];
+        partial[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) partial[nb] = tot;
+}
+
+// out[i] = exclusive prefix of f over [0, i); out[n] = total.
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_scan_apply(F f, uint64_t n, const uint64_t* partial, uint64_t nb,
+                                                       uint64_t* out) {
+    __shared__ uint64_t v[kScanBlock];
+    const uint64_t base = blockIdx.x * kScanBlock;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {  // coalesced reads, staged in LDS
+        const uint32_t k = j * kBlock + threadIdx.x;
+        v[k] = (base + k < n) ? f(base + k) : 0;
+    }
+    __syncthreads();
+    uint64_t loc[kScanItems];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        loc[j] = s;
+        s += v[threadIdx.x * kScanItems + j];
+    }
+    uint64_t tot;
+    const uint64_t pre = block_exclusive_scan(s, &tot) + partial[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) v[threadIdx.x * kScanItems + j] = pre + loc[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {  // coalesced writes
+        const uint32_t k = j * kBlock + threadIdx.x;
+        if (base + k < n) out[base + k] = v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = partial[nb];
+}
+
+// ---- record / chunk location -------------------------------------------------
+// Largest r in [0, n] with offs[r] <= p (offs non-decreasing).  For a byte
+// position p < offs[n] this is the record whose bytes cover p (records of
+// zero length are skipped).
+__device__ __forceinline__ uint64_t upper_index(const uint64_t* offs, uint64_t n, uint64_t p) {
+    uint64_t lo = 0, hi = n;  // invariant: offs[lo] <= p, answer in [lo, hi]
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (offs[mid] <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Per-tile helper: the tile's first covering record, then a window of the
+// following record starts in LDS.
+struct Window {
+    uint64_t r0;
+    uint32_t len;  // entries valid in win[0..len)
+};
+
+__device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, uint64_t lo, uint64_t* win,
+                                              uint64_t* shared_r0) {
+    if (threadIdx.x == 0) *shared_r0 = upper_index(offs, n, lo);
+    __syncthreads();
+    const uint64_t r0 = *shared_r0;
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(kWindow, n + 1 - r0));
+    for (uint32_t k = threadIdx.x; k < len; k += kBlock) win[k] = offs[r0 + k];
+    __syncthreads();
+    return {r0, len};
+}
+
+// Covering record of byte p using the window (global search when p lies past it).
+__device__ __forceinline__ uint64_t find_record(const uint64_t* offs, uint64_t n, const Window& w,
+                                                const uint64_t* win, uint64_t p) {
+    if (win[w.len - 1] <= p) {
+        if (w.r0 + w.len - 1 >= n) return n;
+        return upper_index(offs, n, p);  // rare: window exhausted
+    }
+    uint32_t lo = 0, hi = w.len - 1;  // win[lo] <= p < win[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (win[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    return w.r0 + lo;
+}
+
+// ---- pack ---------------------------------------------------------------------
+// Write `cnt` bytes of record r starting at byte q of the record into dst (LDS).
+__device__ void emit_record_bytes(const VarArgs& a, const uint8_t* pre, uint64_t r, uint64_t q, uint32_t cnt,
+                                  uint8_t* dst) {
+    uint64_t s = 0;  // start of the current segment within the record
+    const uint64_t end = q + cnt;
+    // prefix
+    for (; q < end && q < a.prefix_len; ++q) *dst++ = pre[q];
+    s = a.prefix_len;
+    for (uint32_t f = 0; f < a.nfields && q < end; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            const uint8_t* src = a.col[f] + r * sz;
+            for (; q < end && q < s + sz; ++q) *dst++ = src[q - s];
+            s += sz;
+        } else {
+            const uint64_t b = a.soff[f][r], len = a.soff[f][r + 1] - b;
+            for (; q < end && q < s + 8; ++q) *dst++ = static_cast<uint8_t>(len >> (8 * (q - s)));
+            s += 8;
+            const uint8_t* src = a.col[f] + b;
+            for (; q < end && q < s + len; ++q) *dst++ = src[q - s];
+            s += len;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* __restrict__ rec_offs, uint64_t n,
+                                                     uint8_t* __restrict__ wire, uint64_t wire_cap,
+                                                     srpc_unpack_status* st) {
+    __shared__ uint64_t win[kWindow];
+    __shared__ uint64_t r0s;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 16];
+    __shared__ uint8_t pre[kMaxPrefix];
+    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
+    const uint64_t total = rec_offs[n];
+    const uint64_t limit = min(total, wire_cap);
+    if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
+        report_bad(st, SRPC_STATUS_BOUNDS, upper_index(rec_offs, n, wire_cap));
+    const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t lo = t * kTileBytes;
+        const Window w = load_window(rec_offs, n, lo, win, &r0s);
+        const uint64_t p0 = lo + 16ull * threadIdx.x;
+        if (p0 < limit) {
+            const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
+            uint8_t* slot = stage + 16 * threadIdx.x;
+            uint64_t r = find_record(rec_offs, n, w, win, p0);
+            uint64_t p = p0;
+            uint32_t b = 0;
+            while (b < nb && r < n) {
+                const uint64_t rs = rec_offs[r], re = rec_offs[r + 1];
+                const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
+                emit_record_bytes(a, pre, r, p - rs, cnt, slot + b);
+                b += cnt;
+                p += cnt;
+                ++r;
+            }
+            if (nb == 16) {
+                *reinterpret_cast<uint4*>(wire + p0) = *reinterpret_cast<const uint4*>(slot);
+            } else {
+                for (uint32_t i = 0; i < nb; ++i) wire[p0 + i] = slot[i];
+            }
+        }
+        __syncthreads();  // the window is rewritten for the next tile
+    }
+}
+
+// ---- unpack -------------------------------------------------------------------
+__device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* p) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= static_cast<uint64_t>(p[i]) << (8 * i);
+    return v;
+}
+
+// lens/spos: [nstrings][n] scratch.  Errors zero the record's string lengths.
+__global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
+                                                            uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
+                                                            uint64_t n, uint64_t* lens, uint64_t* spos,
+                                                            srpc_unpack_status* st) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t start = rec_offs[r], end = rec_offs[r + 1];
+    uint32_t flag = 0;
+    if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
+    uint64_t pos = start + a.prefix_len;
+    if (!flag) {
+        for (uint32_t i = 0; i < a.prefix_len; ++i)
+            if (wire[start + i] != a.prefix[i]) {
+                flag = SRPC_STATUS_PREFIX;
+                break;
+            }
+    }
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            pos += sz;
+            continue;
+        }
+        const uint32_t si = a.sidx[f];
+        uint64_t len = 0;
+        if (flag != SRPC_STATUS_BOUNDS && pos + 8 <= end) {
+            len = load_u64_unaligned(wire + pos);
+            pos += 8;
+            if (len > end - pos) {  // the reference checks after the read (core.hpp:29-31)
+                flag = SRPC_STATUS_BOUNDS;
+                len = 0;
+            }
+        } else {
+            flag = SRPC_STATUS_BOUNDS;
+        }
+        spos[si * n + r] = pos;
+        lens[si * n + r] = len;
+        pos += len;
+    }
+    if (!flag && pos != end) flag = SRPC_STATUS_BOUNDS;  // record size disagrees with the index
+    if (flag == SRPC_STATUS_BOUNDS)  // positions are untrustworthy: decode nothing of this record's strings
+        for (uint32_t si = 0; si < a.nstrings; ++si) lens[si * n + r] = 0;
+    if (flag && st) report_bad(st, flag, r);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_var_fixed(VarArgs a, const uint8_t* __restrict__ wire,
+                                                             const uint64_t* __restrict__ rec_offs, uint64_t n,
+                                                             const uint64_t* lens) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (r >= n) return;
+    uint64_t pos = rec_offs[r] + a.prefix_len;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz == 0) {
+            pos += 8 + lens[a.sidx[f] * n + r];
+            continue;
+        }
+        uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
+        const uint8_t* src = wire + pos;
+        switch (sz) {
+        case 1: dst[0] = src[0]; break;
+        case 2: { uint16_t v = src[0] | (src[1] << 8); *reinterpret_cast<uint16_t*>(dst) = v; break; }
+        case 4: {
+            uint32_t v = 0;
+            for (int i = 0; i < 4; ++i) v |= static_cast<uint32_t>(src[i]) << (8 * i);
+            *reinterpret_cast<uint32_t*>(dst) = v;
+            break;
+        }
+        default: *reinterpret_cast<uint64_t*>(dst) = load_u64_unaligned(src); break;
+        }
+        pos += sz;
+    }
+}
+
+// Chars of one string field: output chunk c = bytes [16c, 16c+16) of chars.
+__global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire,
+                                                             const uint64_t* __restrict__ soff,
+                                                             const uint64_t* __restrict__ spos, uint64_t n,
+                                                             uint8_t* __restrict__ chars) {
+    __shared__ uint64_t win[kWindow];
+    __shared__ uint64_t r0s;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 16];
+    const uint64_t total = soff[n];
+    const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t lo = t * kTileBytes;
+        const Window w = load_window(soff, n, lo, win, &r0s);
+        const uint64_t p0 = lo + 16ull * threadIdx.x;
+        if (p0 < total) {
+            const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
+            uint8_t* slot = stage + 16 * threadIdx.x;
+            uint64_t r = find_record(soff, n, w, win, p0);
+            uint64_t p = p0;
+            uint32_t b = 0;
+            while (b < nb && r < n) {
+                const uint64_t rs = soff[r], re = soff[r + 1];
+                const uint64_t cnt = min<uint64_t>(nb - b, re - p);
+                const uint8_t* src = wire + spos[r] + (p - rs);
+                for (uint64_t i = 0; i < cnt; ++i) slot[b + i] = src[i];
+                b += static_cast<uint32_t>(cnt);
+                p += cnt;
+                ++r;
+            }
+            if (nb == 16) {
+                *reinterpret_cast<uint4*>(chars + p0) = *reinterpret_cast<const uint4*>(slot);
+            } else {
+                for (uint32_t i = 0; i < nb; ++i) chars[p0 + i] = slot[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_reset_status(srpc_unpack_status* st) {
+    if (threadIdx.x == 0) {
+        st->flags = 0;
+        st->reserved = 0;
+        st->first_bad_record = ~0ull;
+    }
+}
+
+// ---- host helpers -------------------------------------------------------------
+uint64_t scan_blocks(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
+
+template <class F>
+int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, hipStream_t s) {
+    const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
+    if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb);
+    hipLaunchKernelGGL(k_scan_apply<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, nb, out);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+VarArgs make_var_args(const srpc_plan* p, const void* const* cols, const uint64_t* const* str_offs) {
+    VarArgs a{};
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        a.col[f] = static_cast<const uint8_t*>(cols[f]);
+        a.size[f] = p->size[f];
+        if (p->size[f] == 0) {
+            a.soff[f] = str_offs ? str_offs[f] : nullptr;
+            a.sidx[f] = si++;
+        }
+    }
+    a.prefix = p->d_prefix;
+    a.nfields = p->nfields;
+    a.nstrings = p->nstrings;
+    a.prefix_len = p->prefix_len;
+    a.fixed_bytes = p->fixed_bytes;
+    return a;
+}
+
+// scratch layout: [partials: nb+1 u64] ... (unpack) [lens: ns*n u64] [spos: ns*n u64]
+uint64_t scratch_need(const srpc_plan* p, uint64_t n, bool unpack) {
+    const uint64_t part = 8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1);
+    uint64_t b = (part + 255) & ~255ull;
+    if (unpack) b += 2 * 8 * static_cast<uint64_t>(p->nstrings) * n;
+    return b;
+}
+
+}  // namespace
+}  // namespace srpc_impl
+
+using namespace srpc_impl;
+
+extern "C" {
+
+int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t* out) {
+    if (!p || !out) return SRPC_E_INVALID;
+    if (!p->has_string) {
+        *out = 0;
+        return SRPC_OK;
+    }
+    *out = std::max(scratch_need(p, n, false), scratch_need(p, n, true));
+    return SRPC_OK;
+}
+
+int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_t* const* str_offs, uint64_t n,
+                      uint8_t* wire, uint64_t wire_cap, uint64_t* rec_offs, srpc_unpack_status* st,
+                      void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (!p || !p->has_string) return SRPC_E_INVALID;
+    auto s = static_cast<hipStream_t>(stream);
+    if (st) {
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st);
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    }
+    if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
+    if (scratch_bytes < scratch_need(p, n, false)) return SRPC_E_CAPACITY;
+    if (!aligned(wire, 16) || !aligned(rec_offs, 8) || !aligned(scratch, 8)) return SRPC_E_ALIGN;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (!cols[f]) return SRPC_E_INVALID;
+        if (p->size[f] == 0 && (!str_offs[f] || !aligned(str_offs[f], 8))) return SRPC_E_INVALID;
+    }
+    const VarArgs a = make_var_args(p, cols, str_offs);
+    int rc = launch_scan(PackSizes{a}, n, static_cast<uint64_t*>(scratch), rec_offs, s);
+    if (rc) return rc;
+    if (n == 0) return SRPC_OK;
+    if (!wire) return SRPC_E_INVALID;
+    hipLaunchKernelGGL(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, wire, wire_cap, st);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                        const uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                        srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (!p || !p->has_string) return SRPC_E_INVALID;
+    auto s = static_cast<hipStream_t>(stream);
+    if (st) {
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st);
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    }
+    if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
+    if (scratch_bytes < scratch_need(p, n, true)) return SRPC_E_CAPACITY;
+    if (!aligned(scratch, 8) || !aligned(rec_offs, 8)) return SRPC_E_ALIGN;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (!cols[f]) return SRPC_E_INVALID;
+        if (p->size[f] && !aligned(cols[f], p->size[f])) return SRPC_E_ALIGN;
+        if (p->size[f] == 0 && (!str_offs[f] || !aligned(str_offs[f], 8) || !aligned(cols[f], 16)))
+            return SRPC_E_ALIGN;
+    }
+    const VarArgs a = make_var_args(p, reinterpret_cast<const void* const*>(cols),
+                                    reinterpret_cast<const uint64_t* const*>(str_offs));
+    auto* partial = static_cast<uint64_t*>(scratch);
+    const uint64_t part = 8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1);
+    auto* lens = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) + ((part + 255) & ~255ull));
+    uint64_t* spos = lens + static_cast<uint64_t>(p->nstrings) * n;
+    const uint64_t grid = (n + kBlock - 1) / kBlock;
+    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    if (n) {
+        if (!wire) return SRPC_E_INVALID;
+        hipLaunchKernelGGL(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+                           wire_len, rec_offs, n, lens, spos, st);
+    }
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (p->size[f]) continue;
+        int rc = launch_scan(ArrayVals{lens + a.sidx[f] * n}, n, partial, str_offs[f], s);
+        if (rc) return rc;
+    }
+    if (n == 0) return SRPC_OK;
+    hipLaunchKernelGGL(k_unpack_var_fixed, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, rec_offs,
+                       n, lens);
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (p->size[f]) continue;
+        hipLaunchKernelGGL(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, str_offs[f],
+                           spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
+    }
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+}  // extern "C"

@@ -165,6 +165,38 @@ class GpuPacker:
                                                 _dptr(status), _stream(stream)),
                      "srpc_gpu_unpack")
 
+    # -- string schemas (SRPC_PATH_VAR) -------------------------------------
+    def var_scratch_bytes(self, n: int) -> int:
+        out = C.c_uint64()
+        check(_lib.lib().srpc_plan_var_scratch_bytes(self._h, n, C.byref(out)),
+              "srpc_plan_var_scratch_bytes")
+        return out.value
+
+    def _str_offs(self, str_offs: Sequence) -> C.Array:
+        ptrs = [_dptr(o) if (o is not None and k == STRING) else 0
+                for o, k in zip(str_offs, self.schema.kinds)]
+        return (C.c_void_p * len(ptrs))(*ptrs)
+
+    def pack_var(self, cols: Sequence, str_offs: Sequence, n: int, wire, wire_cap: int, rec_offs,
+                 scratch, scratch_bytes: int, status=None, stream=None) -> None:
+        """Pack n records with string fields; writes rec_offs[0..n] (async).
+        ``str_offs[f]``: n+1 u64 device offsets for string fields, None otherwise."""
+        check(_lib.lib().srpc_gpu_pack_var(self._h, self._cols(cols), self._str_offs(str_offs), n,
+                                           _dptr(wire), wire_cap, _dptr(rec_offs), _dptr(status),
+                                           _dptr(scratch), scratch_bytes, _stream(stream)),
+              "srpc_gpu_pack_var")
+
+    def unpack_var(self, wire, wire_len: int, n: int, rec_offs, cols: Sequence, str_offs: Sequence,
+                   scratch, scratch_bytes: int, status=None, stream=None) -> None:
+        """Unpack n records whose starts are rec_offs[0..n] (async).  String
+        field f's chars go to cols[f] (room for wire_len bytes), its n+1
+        offsets to str_offs[f]."""
+        check(_lib.lib().srpc_gpu_unpack_var(self._h, _dptr(wire), wire_len, n, _dptr(rec_offs),
+                                             self._cols(cols), self._str_offs(str_offs),
+                                             _dptr(status), _dptr(scratch), scratch_bytes,
+                                             _stream(stream)),
+              "srpc_gpu_unpack_var")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.lib().srpc_plan_destroy(self._h)

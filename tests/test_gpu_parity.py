@@ -300,3 +300,181 @@ def test_quad_full_size_digest_and_roundtrip(manifest, label):
     p.pack(cols, n, wire2)
     torch.cuda.synchronize()
     assert torch.equal(wire, wire2)
+
+
+# ---- string fields (SRPC_PATH_VAR) -------------------------------------------------
+
+MULTIPLE = Schema.of("multiple_primitives", ("arg1", "int8"), ("arg2", "char"), ("arg3", "int64"),
+                     ("arg4", "string"))
+
+
+def _dev_u64(a):
+    return dev(np.ascontiguousarray(a, dtype=np.uint64))
+
+
+def gpu_pack_var(p, kinds, cols, offs, n):
+    """cols[f]: numpy column (fixed) or uint8 chars (string); offs[f]: n+1 offsets or None."""
+    dcols = [dev(c) for c in cols]
+    doffs = [_dev_u64(o) if o is not None else None for o in offs]
+    total = int(sum(int(o[n] - o[0]) for o in offs if o is not None)) + n * (
+        len(p.prefix) + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds))
+    wire = empty(total + 16)
+    rec = empty(8 * (n + 1))
+    sb = p.var_scratch_bytes(n)
+    scratch = empty(sb + 16)
+    st = status_buf()
+    p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, st)
+    rec_h = host(rec, 8 * (n + 1), np.uint64)
+    return host(wire, total).tobytes(), rec_h, read_status(st)
+
+
+def gpu_unpack_var(p, kinds, wire: bytes, n, rec_offs, wire_len=None):
+    w = dev(np.frombuffer(wire, np.uint8)) if len(wire) else empty(16)
+    L = len(wire) if wire_len is None else wire_len
+    outs, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            outs.append(empty(L + 16))
+            offs.append(empty(8 * (n + 1)))
+        else:
+            outs.append(empty(n * oracle.KIND_SIZE[k] + 16))
+            offs.append(None)
+    sb = p.var_scratch_bytes(n)
+    scratch = empty(sb + 16)
+    st = status_buf()
+    p.unpack_var(w, L, n, _dev_u64(rec_offs), outs, offs, scratch, sb, st)
+    res = []
+    res_offs = []
+    for k, o, so in zip(kinds, outs, offs):
+        if k == oracle.STRING:
+            oh = host(so, 8 * (n + 1), np.uint64)
+            res_offs.append(oh)
+            res.append(host(o, int(oh[n])) if n else np.zeros(0, np.uint8))
+        else:
+            res_offs.append(None)
+            res.append(host(o, n * oracle.KIND_SIZE[k], oracle.KIND_DTYPE[k]))
+    return res, res_offs, read_status(st)
+
+
+def _rec_offsets(kinds, offs, n, prefix_len=0):
+    fixed = prefix_len + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds)
+    sizes = np.full(n, fixed, np.uint64)
+    for k, o in zip(kinds, offs):
+        if k == oracle.STRING:
+            sizes += np.diff(o.astype(np.uint64))
+    r = np.zeros(n + 1, np.uint64)
+    r[1:] = np.cumsum(sizes)
+    return r
+
+
+def test_strings_reference_fixture(golden_dir):
+    z = np.load(os.path.join(golden_dir, "multiple_strings_in.npz"))
+    kinds = MULTIPLE.kinds
+    cols = [z["a1"], z["a2"], z["a3"], z["chars"]]
+    offs = [None, None, None, z["offs"]]
+    n = len(z["a1"])
+    p = GpuPacker(MULTIPLE)
+    assert p.path == srpc_amd.SRPC_PATH_VAR and p.record_bytes == 0
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st == (0, 2**64 - 1)
+    assert wire == read(golden_dir, "multiple_strings.bin")
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
+    back, boffs, st = gpu_unpack_var(p, kinds, wire, n, rec)
+    assert st == (0, 2**64 - 1)
+    for a, b in zip(cols[:3], back[:3]):
+        assert a.tobytes() == b.tobytes()
+    assert np.array_equal(boffs[3], z["offs"]) and back[3].tobytes() == z["chars"].tobytes()
+
+
+def _random_string_batch(kinds, n, rng, maxlen):
+    cols, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            lens = rng.integers(0, maxlen + 1, n).astype(np.uint64)
+            lens[rng.random(n) < 0.2] = 0  # plenty of empty strings
+            o = np.zeros(n + 1, np.uint64)
+            o[1:] = np.cumsum(lens)
+            cols.append(rng.integers(0, 256, max(1, int(o[-1])), dtype=np.uint8))
+            offs.append(o)
+        else:
+            dt = np.dtype(oracle.KIND_DTYPE[k])
+            c = rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt)
+            cols.append((c & 1).astype(np.uint8) if k == oracle.BOOL else c)
+            offs.append(None)
+    return cols, offs
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 2047, 2048, 2049, 30_001])
+@pytest.mark.parametrize("schema,maxlen,envelope", [
+    ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
+    ("nested", 64, "response")])
+def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
+    kinds = {"s": [oracle.STRING],
+             "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
+             "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
+             "nested": [oracle.INT64, oracle.INT8, oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]}[schema]
+    if maxlen > 1000 and n > 3000:
+        n = 3000
+    rng = np.random.default_rng(n + maxlen)
+    cols, offs = _random_string_batch(kinds, n, rng, maxlen)
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    if envelope == "request":
+        p = GpuPacker.for_request(sch, "Svc_servicer::m")
+    elif envelope == "response":
+        p = GpuPacker.for_response(sch, 2)
+    else:
+        p = GpuPacker(sch)
+    want = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st[0] == 0
+    assert wire == want
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
+    back, boffs, st = gpu_unpack_var(p, kinds, want, n, rec)
+    assert st[0] == 0
+    rc, ocols, ooffs, _, _ = oracle.unpack(kinds, want, n, p.prefix)
+    assert rc == 0
+    for f, k in enumerate(kinds):
+        assert back[f].tobytes() == ocols[f].tobytes(), f
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f], ooffs[f])
+
+
+def test_strings_errors():
+    kinds = [oracle.INT32, oracle.STRING]
+    n = 1000
+    rng = np.random.default_rng(5)
+    cols, offs = _random_string_batch(kinds, n, rng, 30)
+    p = GpuPacker.for_request(Schema("E", (("x", oracle.INT32), ("s", oracle.STRING))), "Svc::m")
+    wire = bytearray(oracle.pack(kinds, cols, n, p.prefix, list(offs)))
+    rec = _rec_offsets(kinds, offs, n, len(p.prefix))
+    # a length field pointing past its record
+    bad = 417
+    pos = int(rec[bad]) + len(p.prefix) + 4
+    wire[pos:pos + 8] = (10**6).to_bytes(8, "little")
+    _, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
+    assert st == (srpc_amd.SRPC_STATUS_BOUNDS, bad)
+    # prefix mismatch (method name) in a later record, length bug fixed
+    wire[pos:pos + 8] = int(offs[1][bad + 1] - offs[1][bad]).to_bytes(8, "little")
+    wire[int(rec[700]) + 9] ^= 0x40
+    back, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
+    assert st == (SRPC_STATUS_PREFIX, 700)
+    assert np.array_equal(back[0], cols[0])  # fields still decoded
+    # an index that disagrees with the record sizes
+    rec2 = rec.copy()
+    rec2[5] += 1
+    _, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec2)
+    assert st[0] & srpc_amd.SRPC_STATUS_BOUNDS and st[1] == 4
+    # pack into too small a buffer: bounds flagged at the first record that does not fit
+    dcols = [dev(c) for c in cols]
+    doffs = [None, _dev_u64(offs[1])]
+    recd = empty(8 * (n + 1))
+    sb = p.var_scratch_bytes(n)
+    scratch = empty(sb + 16)
+    s = status_buf()
+    small = int(rec[600]) + 3
+    w = empty(int(rec[n]) + 16)
+    p.pack_var(dcols, doffs, n, w, small, recd, scratch, sb, s)
+    assert read_status(s) == (srpc_amd.SRPC_STATUS_BOUNDS, 600)
+    got = host(w, int(rec[n])).tobytes()
+    assert got[:small] == bytes(oracle.pack(kinds, cols, n, p.prefix, list(offs)))[:small]
+    assert set(got[small:]) <= {0xA5}
