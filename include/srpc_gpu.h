@@ -116,12 +116,14 @@ int srpc_plan_path(const srpc_plan* plan, int* out);
  * (SRPC_PATH_TILE is valid for every fixed schema). */
 int srpc_plan_force_path(srpc_plan* plan, int path);
 
-/* Performance knobs of the DWORD path (defaults are the measured best on
+/* Performance knobs (defaults are the measured best on
  * MI355X; results are identical for every setting). */
 #define SRPC_TUNE_RECORDS_PER_LANE 1 /* 1 or 4 (4: 16-byte column loads, needs 4-byte
                                         fields and 16-byte aligned columns) */
 #define SRPC_TUNE_ITER 2             /* records (or quads) per lane per launch: 1,2,4,8 */
 #define SRPC_TUNE_NONTEMPORAL 3      /* bit0 non-temporal stores, bit1 loads      */
+#define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
+                                        (1024..49152)                            */
 int srpc_plan_tune(srpc_plan* plan, int knob, int value);
 
 /* Pack n records.  d_cols[f] (host array of nfields device pointers) holds

@@ -567,6 +567,49 @@ int check_cols(const srpc_plan* p, const void* const* cols, uint64_t n) {
     return SRPC_OK;
 }
 
+// DWORD variant per record width, from the interleaved A/B sweeps of
+// profiles/r01_sweep_{quad,number,two}.log and the bench loop (r01_tune.log):
+// 1-dword records want 16-byte column loads (4 records per lane); 2-dword
+// records two records per lane-iteration with non-temporal loads; 4-dword
+// records one per lane with non-temporal loads and stores.
+DwordVariant default_dword_variant(uint32_t W) {
+    DwordVariant v;
+    if (W == 1) {
+        v.rpl = 4;
+        v.iter = 1;
+        v.nt = kNtLoad;
+    } else if (W == 4) {
+        v.rpl = 1;
+        v.iter = 1;
+        v.nt = kNtLoad | kNtStore;
+    } else {
+        v.rpl = 1;
+        v.iter = 2;
+        v.nt = kNtLoad;
+    }
+    return v;
+}
+
+// TILE geometry: R records per tile (a multiple of 16, so every tile's wire
+// span is 16-byte aligned) with an image of about `target` bytes, the
+// template period L = lcm(stride, 16), and a grid-stride grid of as many
+// workgroups as can be resident.
+void configure_tile(srpc_plan* p, uint32_t target) {
+    const uint32_t S = static_cast<uint32_t>(p->stride);
+    const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
+    p->tile_R = R;
+    p->tile_L = S / gcd_u32(S, 16) * 16;
+    p->tile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
+    int per_cu = 0, cus = 0;
+    DeviceGuard g(p->device);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_tile, kBlock, p->tile_lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) {
+        per_cu = 4;
+        cus = 256;
+    }
+    p->tile_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -636,14 +679,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
     p->stride = o;
     p->all4 = all4_fields;
     p->dword_ok = dword_ok && (o / 4) <= static_cast<uint64_t>(kMaxDwords);
-    if (o <= kMaxTileStride) {
-        const uint32_t S = static_cast<uint32_t>(o);
-        uint32_t R = 16 * std::max<uint32_t>(1, kTileTarget / (16 * S));
-        p->tile_R = R;
-        p->tile_L = S / gcd_u32(S, 16) * 16;  // lcm(S, 16)
-        p->tile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
-    }
-    p->path = p->dword_ok ? SRPC_PATH_DWORD : (p->tile_R ? SRPC_PATH_TILE : 0);
+    p->path = p->dword_ok ? SRPC_PATH_DWORD : (o <= kMaxTileStride ? SRPC_PATH_TILE : 0);
     if (!p->path) {
         delete p;
         return SRPC_E_UNSUPPORTED;
@@ -657,16 +693,10 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             return SRPC_E_HIP;
         }
     }
-    if (p->tile_R) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_tile, kBlock, p->tile_lds) !=
-                hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
-            per_cu = 4;
-            cus = 256;
-        }
-        p->tile_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
-    }
+    if (p->dword_ok) p->dv = default_dword_variant(static_cast<uint32_t>(o / 4));
+    // TILE image size: the best of 4-48 KiB per record width on MI355X
+    // (profiles/r01_sweep_tile.log): 16 KiB for narrow records, 32 KiB for wide.
+    if (o <= kMaxTileStride) configure_tile(p, o >= 32 ? 32768 : 16384);
     *out = p;
     return SRPC_OK;
 }
@@ -720,6 +750,10 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
     case SRPC_TUNE_NONTEMPORAL:
         if (value < 0 || value > 3) return SRPC_E_INVALID;
         p->dv.nt = value;
+        return SRPC_OK;
+    case SRPC_TUNE_TILE_BYTES:
+        if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
+        configure_tile(p, static_cast<uint32_t>(value));
         return SRPC_OK;
     default: return SRPC_E_INVALID;
     }

@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Throughput of every kernel family on representative schemas (one MI355X).
+
+For each case: pack and unpack of N records through the C ABI, timed with
+HIP events on the launch stream (median of R reps after warm-up), reported
+as algorithmic GB/s (columns + wire bytes moved once) and fraction of the
+8 TB/s HBM3E peak.  Every case is first checked bit-exact against the CPU
+oracle on a 4096-record prefix of the same inputs.
+
+    python tools/bench_paths.py [--reps 20] [--out gpurun_out/paths.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import oracle
+    import srpc_amd
+    from srpc_amd import NUMBER, QUAD, SQUARE_METHOD, GpuPacker, Schema
+
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream()
+    rows = []
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(args.reps):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            fn()
+            b.record(s)
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) / 1e3)
+        return statistics.median(ts)
+
+    def t_u8(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(dev)
+
+    def fixed_case(name, sch, n, prefix=b"", path=None):
+        p = GpuPacker(sch, prefix)
+        if path:
+            p.force_path(path)
+        rng = np.random.default_rng(1)
+        cols = []
+        for k in sch.kinds:
+            dt = np.dtype(oracle.KIND_DTYPE[k])
+            c = rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt)
+            cols.append((c & 1).astype(np.uint8) if k == oracle.BOOL else c)
+        dcols = [t_u8(c) for c in cols]
+        wire = torch.empty(n * p.record_bytes + 16, dtype=torch.uint8, device=dev)
+        back = [torch.empty_like(c) for c in dcols]
+        p.pack(dcols, n, wire, stream=s)
+        torch.cuda.synchronize()
+        m = 4096
+        ok = wire[: m * p.record_bytes].cpu().numpy().tobytes() == oracle.pack(
+            sch.kinds, [c[:m] for c in cols], m, prefix)
+        col_bytes = sum(c.nbytes for c in cols)
+        alg = col_bytes + n * p.record_bytes
+        tp = timeit(lambda: p.pack(dcols, n, wire, stream=s))
+        tu = timeit(lambda: p.unpack(wire, n * p.record_bytes, n, back, stream=s))
+        ok = ok and all(torch.equal(a, b) for a, b in zip(dcols, back))
+        rows.append({"case": name, "path": {1: "dword", 2: "tile", 3: "var"}[p.path], "records": n,
+                     "record_bytes": p.record_bytes, "alg_bytes": alg, "pack_us": round(tp * 1e6, 2),
+                     "unpack_us": round(tu * 1e6, 2), "pack_GBps": round(alg / tp / 1e9, 1),
+                     "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
+                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
+
+    def var_case(name, kinds, n, maxlen, prefix=b""):
+        sch = Schema("V", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+        p = GpuPacker(sch, prefix)
+        rng = np.random.default_rng(2)
+        cols, offs = [], []
+        for k in kinds:
+            if k == oracle.STRING:
+                lens = rng.integers(0, maxlen + 1, n).astype(np.uint64)
+                o = np.zeros(n + 1, np.uint64)
+                o[1:] = np.cumsum(lens)
+                cols.append(rng.integers(0, 256, int(o[-1]) + 1, dtype=np.uint8))
+                offs.append(o)
+            else:
+                dt = np.dtype(oracle.KIND_DTYPE[k])
+                cols.append(rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt))
+                offs.append(None)
+        fixed = len(prefix) + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds)
+        total = n * fixed + int(sum(int(o[-1]) for o in offs if o is not None))
+        dcols = [t_u8(c) for c in cols]
+        doffs = [t_u8(o) if o is not None else None for o in offs]
+        wire = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+        rec = torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev)
+        sb = p.var_scratch_bytes(n)
+        scratch = torch.empty(sb + 16, dtype=torch.uint8, device=dev)
+        outs = [torch.empty(total + 16 if k == oracle.STRING else n * oracle.KIND_SIZE[k] + 16,
+                            dtype=torch.uint8, device=dev) for k in kinds]
+        ooffs = [torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev) if k == oracle.STRING else None
+                 for k in kinds]
+        p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s)
+        torch.cuda.synchronize()
+        want = oracle.pack(kinds, cols, n, prefix, list(offs))
+        ok = wire[:total].cpu().numpy().tobytes() == want
+        col_bytes = sum(c.nbytes for c, k in zip(cols, kinds) if k != oracle.STRING)
+        str_bytes = total - n * fixed
+        alg = col_bytes + str_bytes + 8 * (n + 1) * sum(k == oracle.STRING for k in kinds) + total
+        tp = timeit(lambda: p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s))
+        tu = timeit(lambda: p.unpack_var(wire, total, n, rec, outs, ooffs, scratch, sb, stream=s))
+        rows.append({"case": name, "path": "var", "records": n, "wire_bytes": total, "alg_bytes": alg,
+                     "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
+                     "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
+                     "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
+                     "parity_ok": bool(ok)})
+
+    N = 1 << 24
+    fixed_case("quad_dword_16M", QUAD, N)
+    fixed_case("quad_tile_16M", QUAD, N, path=srpc_amd.SRPC_PATH_TILE)
+    fixed_case("number_body_16M", NUMBER, N)
+    fixed_case("all_kinds_17B_16M", Schema.of("all_kinds", ("a", "bool"), ("b", "int8"), ("c", "char"),
+                                              ("d", "int16"), ("e", "int32"), ("f", "int64")), N)
+    fixed_case("square_request_53B_16M", NUMBER, N, srpc_amd.request_prefix(SQUARE_METHOD, "Number"))
+    fixed_case("square_response_19B_16M", NUMBER, N, srpc_amd.response_prefix(0, "Number"))
+    var_case("multiple_primitives_str0-64_4M", [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING],
+             1 << 22, 64)
+    var_case("string_0-1024_1M", [oracle.STRING], 1 << 20, 1024)
+    txt = json.dumps(rows, indent=1)
+    if args.out:
+        os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+        with open(args.out, "w") as f:
+            f.write(txt)
+    for r in rows:
+        print(f'{r["case"]:34s} {r["path"]:5s} pack {r["pack_us"]:9.1f} us {r["pack_GBps"]:7.1f} GB/s '
+              f'({r["pack_frac"]:.3f})  unpack {r["unpack_us"]:9.1f} us {r["unpack_GBps"]:7.1f} GB/s '
+              f'({r["unpack_frac"]:.3f})  parity={r["parity_ok"]}')
+
+
+if __name__ == "__main__":
+    main()
