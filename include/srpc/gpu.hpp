@@ -92,21 +92,41 @@ std::vector<uint8_t> response_prefix(rpc_status_code code) {
     return std::vector<uint8_t>(p.data(), p.data() + p.size());
 }
 
-/// Host-side SoA image of a batch: one byte column per flattened fixed field.
+/// Host-side SoA image of a batch: one column per flattened field.  A fixed
+/// field is n little-endian values; a string field is its chars back to back
+/// plus n+1 u64 offsets (the layout srpc_gpu_pack_var / _unpack_var use).
 template <SrpcMessage T>
 struct host_columns {
-    std::vector<std::vector<uint8_t>> col;
+    std::vector<std::vector<uint8_t>> col;   // fixed: values; string: chars
+    std::vector<std::vector<uint64_t>> offs; // string: n+1 offsets; fixed: empty
     uint64_t n = 0;
 
     void scatter(std::vector<T> const& recs) {
         n = recs.size();
         col.clear();
+        offs.clear();
         T probe{};
-        for_each_leaf<T>(probe, [&](const auto& v) { col.emplace_back(n * sizeof(v)); });
+        for_each_leaf<T>(probe, [&](const auto& v) {
+            using F = std::remove_cvref_t<decltype(v)>;
+            if constexpr (std::is_same_v<F, std::string>) {
+                col.emplace_back();
+                offs.emplace_back(1, 0);
+            } else {
+                col.emplace_back(n * sizeof(F));
+                offs.emplace_back();
+            }
+        });
         for (uint64_t i = 0; i < n; ++i) {
             size_t f = 0;
             for_each_leaf<T>(recs[i], [&](const auto& v) {
-                std::memcpy(col[f++].data() + i * sizeof(v), &v, sizeof(v));
+                using F = std::remove_cvref_t<decltype(v)>;
+                if constexpr (std::is_same_v<F, std::string>) {
+                    col[f].insert(col[f].end(), v.begin(), v.end());
+                    offs[f].push_back(col[f].size());
+                } else {
+                    std::memcpy(col[f].data() + i * sizeof(F), &v, sizeof(F));
+                }
+                ++f;
             });
         }
     }
@@ -116,7 +136,13 @@ struct host_columns {
         for (uint64_t i = 0; i < n; ++i) {
             size_t f = 0;
             for_each_leaf<T>(recs[i], [&](auto& v) {
-                std::memcpy(&v, col[f++].data() + i * sizeof(v), sizeof(v));
+                using F = std::remove_cvref_t<decltype(v)>;
+                if constexpr (std::is_same_v<F, std::string>) {
+                    v.assign(reinterpret_cast<const char*>(col[f].data()) + offs[f][i], offs[f][i + 1] - offs[f][i]);
+                } else {
+                    std::memcpy(&v, col[f].data() + i * sizeof(F), sizeof(F));
+                }
+                ++f;
             });
         }
     }
@@ -149,7 +175,9 @@ public:
         if (_plan) srpc_plan_destroy(_plan);
     }
 
+    /// Fixed wire bytes per record; 0 when T has string fields (use the *_var calls).
     uint64_t record_bytes() const { return _rb; }
+    bool has_strings() const { return _rb == 0; }
     uint32_t nfields() const { return _nfields; }
     srpc_plan* plan() const { return _plan; }
 
@@ -161,6 +189,25 @@ public:
     int unpack(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, void* const* d_cols,
                srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
         return srpc_gpu_unpack(_plan, d_wire, wire_len, n, d_cols, d_status, stream);
+    }
+
+    /// String schemas: device scratch needed by pack_var / unpack_var for n records.
+    uint64_t scratch_bytes(uint64_t n) const {
+        uint64_t b = 0;
+        srpc_plan_var_scratch_bytes(_plan, n, &b);
+        return b;
+    }
+    int pack_var(const void* const* d_cols, const uint64_t* const* d_str_offs, uint64_t n, uint8_t* d_wire,
+                 uint64_t wire_cap, uint64_t* d_rec_offs, void* d_scratch, uint64_t scratch_bytes,
+                 srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
+        return srpc_gpu_pack_var(_plan, d_cols, d_str_offs, n, d_wire, wire_cap, d_rec_offs, d_status, d_scratch,
+                                 scratch_bytes, stream);
+    }
+    int unpack_var(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, const uint64_t* d_rec_offs,
+                   void* const* d_cols, uint64_t* const* d_str_offs, void* d_scratch, uint64_t scratch_bytes,
+                   srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
+        return srpc_gpu_unpack_var(_plan, d_wire, wire_len, n, d_rec_offs, d_cols, d_str_offs, d_status, d_scratch,
+                                   scratch_bytes, stream);
     }
 
 private:

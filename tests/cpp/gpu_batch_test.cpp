@@ -8,6 +8,7 @@
 #include <srpc/packer.hpp>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -94,6 +95,93 @@ static int run(srpc::gpu::batch_packer<T>& bp, size_t n, Fill fill, Eq eq, Emit 
     return 0;
 }
 
+struct Text : public srpc::message_base {
+    int8_t a;
+    std::string s;
+    int64_t b;
+    Inner in;
+    std::string t;
+    static constexpr const char* name = "Text";
+    static constexpr auto fields = std::make_tuple(STRUCT_MEMBER(Text, a, "Text::a"), STRUCT_MEMBER(Text, s, "Text::s"),
+                                                   STRUCT_MEMBER(Text, b, "Text::b"), STRUCT_MEMBER(Text, in, "Text::in"),
+                                                   STRUCT_MEMBER(Text, t, "Text::t"));
+};
+
+// String schemas: batch_packer<T>::pack_var / unpack_var against `p << r`.
+static int run_var(srpc::gpu::batch_packer<Text>& bp, size_t n, std::mt19937_64& rng) {
+    std::vector<Text> recs(n);
+    for (size_t i = 0; i < n; ++i) {
+        recs[i].a = static_cast<int8_t>(rng());
+        recs[i].b = static_cast<int64_t>(rng());
+        recs[i].in.tag = static_cast<int8_t>(rng());
+        recs[i].in.small = static_cast<int16_t>(rng());
+        recs[i].s.assign(rng() % 70, 'x');
+        for (auto& c : recs[i].s) c = static_cast<char>(rng());
+        recs[i].t.assign(rng() % 3 == 0 ? 0 : rng() % 500, 'y');
+    }
+    srpc::packer ref;
+    for (auto& r : recs) ref << r;
+    std::vector<uint8_t> want(*ref.buf());
+    srpc::gpu::host_columns<Text> hc;
+    hc.scatter(recs);
+    const size_t F = hc.col.size();
+    std::vector<void*> dcols(F), dback(F);
+    std::vector<uint64_t*> doffs(F, nullptr), dboffs(F, nullptr);
+    for (size_t f = 0; f < F; ++f) {
+        HIPCHECK(hipMalloc(&dcols[f], hc.col[f].size() + 16));
+        HIPCHECK(hipMemcpy(dcols[f], hc.col[f].data(), hc.col[f].size(), hipMemcpyHostToDevice));
+        HIPCHECK(hipMalloc(&dback[f], std::max(hc.col[f].size(), want.size()) + 16));
+        if (!hc.offs[f].empty()) {
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&doffs[f]), 8 * (n + 1)));
+            HIPCHECK(hipMemcpy(doffs[f], hc.offs[f].data(), 8 * (n + 1), hipMemcpyHostToDevice));
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&dboffs[f]), 8 * (n + 1)));
+        }
+    }
+    uint8_t* dw = nullptr;
+    uint64_t* drec = nullptr;
+    void* scratch = nullptr;
+    const uint64_t sb = bp.scratch_bytes(n);
+    HIPCHECK(hipMalloc(&dw, want.size() + 16));
+    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&drec), 8 * (n + 1)));
+    HIPCHECK(hipMalloc(&scratch, sb + 16));
+    std::vector<const uint64_t*> coffs(doffs.begin(), doffs.end());
+    CHECK(bp.pack_var(dcols.data(), coffs.data(), n, dw, want.size(), drec, scratch, sb) == SRPC_OK);
+    std::vector<uint8_t> got(want.size());
+    HIPCHECK(hipMemcpy(got.data(), dw, got.size(), hipMemcpyDeviceToHost));
+    CHECK(got == want);
+    srpc_unpack_status* st = nullptr;
+    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&st), sizeof(*st)));
+    CHECK(bp.unpack_var(dw, want.size(), n, drec, dback.data(), dboffs.data(), scratch, sb, st) == SRPC_OK);
+    srpc_unpack_status hs{};
+    HIPCHECK(hipMemcpy(&hs, st, sizeof(hs), hipMemcpyDeviceToHost));
+    CHECK(hs.flags == 0);
+    srpc::gpu::host_columns<Text> back = hc;
+    for (size_t f = 0; f < F; ++f) {
+        if (!hc.offs[f].empty())
+            HIPCHECK(hipMemcpy(back.offs[f].data(), dboffs[f], 8 * (n + 1), hipMemcpyDeviceToHost));
+        back.col[f].resize(hc.offs[f].empty() ? hc.col[f].size() : back.offs[f][n]);
+        HIPCHECK(hipMemcpy(back.col[f].data(), dback[f], back.col[f].size(), hipMemcpyDeviceToHost));
+    }
+    std::vector<Text> out;
+    back.gather(out);
+    bool same = true;
+    for (size_t i = 0; same && i < n; ++i)
+        same = out[i].a == recs[i].a && out[i].s == recs[i].s && out[i].b == recs[i].b && out[i].in.tag == recs[i].in.tag &&
+               out[i].in.small == recs[i].in.small && out[i].t == recs[i].t;
+    CHECK(same);
+    for (size_t f = 0; f < F; ++f) {
+        (void)hipFree(dcols[f]);
+        (void)hipFree(dback[f]);
+        if (doffs[f]) (void)hipFree(doffs[f]);
+        if (dboffs[f]) (void)hipFree(dboffs[f]);
+    }
+    (void)hipFree(dw);
+    (void)hipFree(drec);
+    (void)hipFree(scratch);
+    (void)hipFree(st);
+    return 0;
+}
+
 int main() {
     std::mt19937_64 rng(42);
     using srpc::gpu::batch_packer;
@@ -136,6 +224,12 @@ int main() {
                            a.c == b.c && a.v == b.v;
                 },
                 [](srpc::packer& p, const Outer& r) { p << r; })) return 2;
+    }
+    {
+        batch_packer<Text> text;
+        CHECK(text.has_strings());
+        for (size_t n : {1ul, 1000ul, 70001ul})
+            if (run_var(text, n, rng)) return 2;
     }
     std::printf("gpu_batch_test: %d passed, %d failed\n", g_pass, g_fail);
     return g_fail ? 1 : 0;
