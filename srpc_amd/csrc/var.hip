@@ -19,11 +19,13 @@
 //      writes them with one 16-byte store.
 // UNPACK (srpc_gpu_unpack_var) -- needs the record start index rec_offs
 //   (produced by pack, or by frame lengths on a socket):
-//   1. k_unpack_var_walk: one record per lane: prefix check, string lengths
-//      and chars positions, record-size consistency (status word on error).
+//   1. k_unpack_var_walk: one record per lane: prefix check, fixed fields to
+//      their columns, string lengths and chars positions, record-size
+//      consistency (status word on error).
 //   2. scans of each string field's lengths -> str_offs[f][0..n].
-//   3. k_unpack_var_fixed: fixed fields to their columns.
-//   4. k_unpack_var_chars: output-chunk-centric copy of string bytes.
+//   3. k_unpack_var_chars: output-chunk-centric copy of string bytes.
+// Byte movement uses unaligned 16-byte loads (one per record segment per
+// 16-byte chunk), never one load per byte.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -206,27 +208,71 @@ __device__ __forceinline__ uint64_t find_record(const uint64_t* offs, uint64_t n
     return w.r0 + lo;
 }
 
+// ---- byte movers ----------------------------------------------------------------
+// gfx950 runs in unaligned-access mode: a 16-byte memcpy from any address is
+// one global_load_dwordx4, to any LDS address one (or a few) ds_write.  Every
+// copy below moves <= 16 bytes with ONE such load, so a chunk costs one load
+// per record segment it touches instead of one per byte.  Sources are never
+// read past their end (`end`): near it the copy falls back to bytes.
+__device__ __forceinline__ void copy_le16(uint8_t* dst, const uint8_t* src, uint32_t k, const uint8_t* end) {
+    if (src + 16 <= end) {
+        uint4 v;
+        __builtin_memcpy(&v, src, 16);
+        __builtin_memcpy(dst, &v, 16);  // dst has 16 bytes of room (32-byte slots)
+    } else {
+        for (uint32_t i = 0; i < k; ++i) dst[i] = src[i];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T load_unaligned(const uint8_t* p) {
+    T v;
+    __builtin_memcpy(&v, p, sizeof(T));
+    return v;
+}
+
 // ---- pack ---------------------------------------------------------------------
-// Write `cnt` bytes of record r starting at byte q of the record into dst (LDS).
-__device__ void emit_record_bytes(const VarArgs& a, const uint8_t* pre, uint64_t r, uint64_t q, uint32_t cnt,
-                                  uint8_t* dst) {
-    uint64_t s = 0;  // start of the current segment within the record
+// Write `cnt` (<= 16) bytes of record r, from byte q of the record, to dst
+// (an LDS slot with 16 bytes of slack after dst).  Segments in wire order:
+// prefix, then every field (fixed value | u64 length, chars).
+__device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_t* pre, const uint64_t* climit,
+                                                  uint64_t n, uint64_t r, uint64_t q, uint32_t cnt, uint8_t* dst) {
     const uint64_t end = q + cnt;
-    // prefix
-    for (; q < end && q < a.prefix_len; ++q) *dst++ = pre[q];
-    s = a.prefix_len;
+    if (q < a.prefix_len) {
+        const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, a.prefix_len) - q);
+        uint4 v;
+        __builtin_memcpy(&v, pre + q, 16);  // pre has 16 bytes of slack
+        __builtin_memcpy(dst, &v, 16);
+        dst += k;
+        q += k;
+    }
+    uint64_t s = a.prefix_len;  // start of the current segment within the record
     for (uint32_t f = 0; f < a.nfields && q < end; ++f) {
         const uint32_t sz = a.size[f];
         if (sz) {
-            const uint8_t* src = a.col[f] + r * sz;
-            for (; q < end && q < s + sz; ++q) *dst++ = src[q - s];
+            if (q < s + sz) {
+                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + sz) - q);
+                copy_le16(dst, a.col[f] + r * sz + (q - s), k, a.col[f] + n * sz);
+                dst += k;
+                q += k;
+            }
             s += sz;
         } else {
-            const uint64_t b = a.soff[f][r], len = a.soff[f][r + 1] - b;
-            for (; q < end && q < s + 8; ++q) *dst++ = static_cast<uint8_t>(len >> (8 * (q - s)));
+            const uint64_t b0 = a.soff[f][r], len = a.soff[f][r + 1] - b0;
+            if (q < s + 8) {
+                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + 8) - q);
+                const uint64_t v = len >> (8 * (q - s));
+                __builtin_memcpy(dst, &v, 8);
+                dst += k;
+                q += k;
+            }
             s += 8;
-            const uint8_t* src = a.col[f] + b;
-            for (; q < end && q < s + len; ++q) *dst++ = src[q - s];
+            if (q < end && q < s + len) {
+                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + len) - q);
+                copy_le16(dst, a.col[f] + b0 + (q - s), k, a.col[f] + climit[f]);
+                dst += k;
+                q += k;
+            }
             s += len;
         }
     }
@@ -237,9 +283,11 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
                                                      srpc_unpack_status* st) {
     __shared__ uint64_t win[kWindow];
     __shared__ uint64_t r0s;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 16];
-    __shared__ uint8_t pre[kMaxPrefix];
+    __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
     for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
+    for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
     const uint64_t total = rec_offs[n];
     const uint64_t limit = min(total, wire_cap);
     if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
@@ -251,14 +299,16 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
-            uint8_t* slot = stage + 16 * threadIdx.x;
+            uint8_t* slot = stage + 32 * threadIdx.x;
             uint64_t r = find_record(rec_offs, n, w, win, p0);
             uint64_t p = p0;
             uint32_t b = 0;
             while (b < nb && r < n) {
-                const uint64_t rs = rec_offs[r], re = rec_offs[r + 1];
+                const uint64_t k = r - w.r0;
+                const uint64_t rs = k + 1 < w.len ? win[k] : rec_offs[r];
+                const uint64_t re = k + 1 < w.len ? win[k + 1] : rec_offs[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                emit_record_bytes(a, pre, r, p - rs, cnt, slot + b);
+                emit_record_bytes(a, pre, climit, n, r, p - rs, cnt, slot + b);
                 b += cnt;
                 p += cnt;
                 ++r;
@@ -274,43 +324,53 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
 }
 
 // ---- unpack -------------------------------------------------------------------
-__device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v |= static_cast<uint64_t>(p[i]) << (8 * i);
-    return v;
-}
-
-// lens/spos: [nstrings][n] scratch.  Errors zero the record's string lengths.
+// One record per lane: prefix check, every string's length and chars position
+// (lens/spos: [nstrings][n] scratch), and the fixed fields straight into their
+// columns.  A string length past the record end (checked BEFORE it is used;
+// the reference checks after the read, core.hpp:29-31) or a record whose size
+// disagrees with the index is a BOUNDS error: that record's strings are
+// decoded as empty.
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
                                                             uint64_t n, uint64_t* lens, uint64_t* spos,
                                                             srpc_unpack_status* st) {
+    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
+    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
+    __syncthreads();
     const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (r >= n) return;
     const uint64_t start = rec_offs[r], end = rec_offs[r + 1];
     uint32_t flag = 0;
     if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
-    uint64_t pos = start + a.prefix_len;
     if (!flag) {
-        for (uint32_t i = 0; i < a.prefix_len; ++i)
-            if (wire[start + i] != a.prefix[i]) {
-                flag = SRPC_STATUS_PREFIX;
-                break;
-            }
+        uint32_t i = 0;
+        for (; i + 8 <= a.prefix_len; i += 8)
+            if (load_unaligned<uint64_t>(wire + start + i) != load_unaligned<uint64_t>(pre + i)) flag = SRPC_STATUS_PREFIX;
+        for (; i < a.prefix_len; ++i)
+            if (wire[start + i] != pre[i]) flag = SRPC_STATUS_PREFIX;
     }
+    uint64_t pos = start + a.prefix_len;
     for (uint32_t f = 0; f < a.nfields; ++f) {
         const uint32_t sz = a.size[f];
         if (sz) {
+            if (flag != SRPC_STATUS_BOUNDS) {
+                uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
+                switch (sz) {
+                case 1: dst[0] = wire[pos]; break;
+                case 2: *reinterpret_cast<uint16_t*>(dst) = load_unaligned<uint16_t>(wire + pos); break;
+                case 4: *reinterpret_cast<uint32_t*>(dst) = load_unaligned<uint32_t>(wire + pos); break;
+                default: *reinterpret_cast<uint64_t*>(dst) = load_unaligned<uint64_t>(wire + pos); break;
+                }
+            }
             pos += sz;
             continue;
         }
         const uint32_t si = a.sidx[f];
         uint64_t len = 0;
         if (flag != SRPC_STATUS_BOUNDS && pos + 8 <= end) {
-            len = load_u64_unaligned(wire + pos);
+            len = load_unaligned<uint64_t>(wire + pos);
             pos += 8;
-            if (len > end - pos) {  // the reference checks after the read (core.hpp:29-31)
+            if (len > end - pos) {
                 flag = SRPC_STATUS_BOUNDS;
                 len = 0;
             }
@@ -327,43 +387,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
     if (flag && st) report_bad(st, flag, r);
 }
 
-__global__ __launch_bounds__(kBlock) void k_unpack_var_fixed(VarArgs a, const uint8_t* __restrict__ wire,
-                                                             const uint64_t* __restrict__ rec_offs, uint64_t n,
-                                                             const uint64_t* lens) {
-    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n) return;
-    uint64_t pos = rec_offs[r] + a.prefix_len;
-    for (uint32_t f = 0; f < a.nfields; ++f) {
-        const uint32_t sz = a.size[f];
-        if (sz == 0) {
-            pos += 8 + lens[a.sidx[f] * n + r];
-            continue;
-        }
-        uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
-        const uint8_t* src = wire + pos;
-        switch (sz) {
-        case 1: dst[0] = src[0]; break;
-        case 2: { uint16_t v = src[0] | (src[1] << 8); *reinterpret_cast<uint16_t*>(dst) = v; break; }
-        case 4: {
-            uint32_t v = 0;
-            for (int i = 0; i < 4; ++i) v |= static_cast<uint32_t>(src[i]) << (8 * i);
-            *reinterpret_cast<uint32_t*>(dst) = v;
-            break;
-        }
-        default: *reinterpret_cast<uint64_t*>(dst) = load_u64_unaligned(src); break;
-        }
-        pos += sz;
-    }
-}
-
 // Chars of one string field: output chunk c = bytes [16c, 16c+16) of chars.
-__global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire,
+__global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                              const uint64_t* __restrict__ soff,
                                                              const uint64_t* __restrict__ spos, uint64_t n,
                                                              uint8_t* __restrict__ chars) {
     __shared__ uint64_t win[kWindow];
     __shared__ uint64_t r0s;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 16];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -372,16 +403,17 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < total) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
-            uint8_t* slot = stage + 16 * threadIdx.x;
+            uint8_t* slot = stage + 32 * threadIdx.x;
             uint64_t r = find_record(soff, n, w, win, p0);
             uint64_t p = p0;
             uint32_t b = 0;
             while (b < nb && r < n) {
-                const uint64_t rs = soff[r], re = soff[r + 1];
-                const uint64_t cnt = min<uint64_t>(nb - b, re - p);
-                const uint8_t* src = wire + spos[r] + (p - rs);
-                for (uint64_t i = 0; i < cnt; ++i) slot[b + i] = src[i];
-                b += static_cast<uint32_t>(cnt);
+                const uint64_t k = r - w.r0;
+                const uint64_t rs = k + 1 < w.len ? win[k] : soff[r];
+                const uint64_t re = k + 1 < w.len ? win[k + 1] : soff[r + 1];
+                const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
+                if (cnt) copy_le16(slot + b, wire + spos[r] + (p - rs), cnt, wire + wire_len);
+                b += cnt;
                 p += cnt;
                 ++r;
             }
@@ -522,11 +554,9 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (rc) return rc;
     }
     if (n == 0) return SRPC_OK;
-    hipLaunchKernelGGL(k_unpack_var_fixed, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, rec_offs,
-                       n, lens);
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
-        hipLaunchKernelGGL(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, str_offs[f],
+        hipLaunchKernelGGL(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
                            spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="", help="substring filter on case names")
     args = ap.parse_args()
 
     import numpy as np
@@ -56,6 +57,8 @@ def main():
         return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(dev)
 
     def fixed_case(name, sch, n, prefix=b"", path=None):
+        if args.only not in name:
+            return
         p = GpuPacker(sch, prefix)
         if path:
             p.force_path(path)
@@ -85,6 +88,8 @@ def main():
                      "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
 
     def var_case(name, kinds, n, maxlen, prefix=b""):
+        if args.only not in name:
+            return
         sch = Schema("V", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
         p = GpuPacker(sch, prefix)
         rng = np.random.default_rng(2)
