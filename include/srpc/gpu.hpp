@@ -191,10 +191,11 @@ public:
         return srpc_gpu_unpack(_plan, d_wire, wire_len, n, d_cols, d_status, stream);
     }
 
-    /// String schemas: device scratch needed by pack_var / unpack_var for n records.
-    uint64_t scratch_bytes(uint64_t n) const {
+    /// String schemas: device scratch needed by pack_var / unpack_var for n
+    /// records and wire_bytes of wire (pack: wire_cap, unpack: wire_len).
+    uint64_t scratch_bytes(uint64_t n, uint64_t wire_bytes) const {
         uint64_t b = 0;
-        srpc_plan_var_scratch_bytes(_plan, n, &b);
+        srpc_plan_var_scratch_bytes(_plan, n, wire_bytes, &b);
         return b;
     }
     int pack_var(const void* const* d_cols, const uint64_t* const* d_str_offs, uint64_t n, uint8_t* d_wire,

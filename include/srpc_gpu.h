@@ -149,9 +149,11 @@ int srpc_gpu_unpack(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_
  * d_str_offs is a host array of nfields device pointers, NULL for fixed fields.
  * Record starts: d_rec_offs, n+1 u64, [0] = 0, [n] = total wire bytes.
  * Both calls need `scratch_bytes` of device scratch (8-byte aligned) from
- * srpc_plan_var_scratch_bytes; like the fixed calls they are stream-ordered
- * and allocate nothing. */
-int srpc_plan_var_scratch_bytes(const srpc_plan* plan, uint64_t n, uint64_t* out);
+ * srpc_plan_var_scratch_bytes(plan, n, wire_bytes), wire_bytes being the
+ * pack call's wire_cap or the unpack call's wire_len; like the fixed calls
+ * they are stream-ordered and allocate nothing. */
+int srpc_plan_var_scratch_bytes(const srpc_plan* plan, uint64_t n, uint64_t wire_bytes,
+                                uint64_t* out);
 
 /* Pack n records (reference: the `p << r` / pack_request loop over records
  * with std::string members, packer.hpp:193-198).  Writes d_rec_offs[0..n]

@@ -40,7 +40,7 @@ SIGNATURES = {
     "srpc_plan_tune": (C.c_int, [_vp, C.c_int, C.c_int]),
     "srpc_gpu_pack": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
     "srpc_gpu_unpack": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp]),
-    "srpc_plan_var_scratch_bytes": (C.c_int, [_vp, _u64, C.POINTER(_u64)]),
+    "srpc_plan_var_scratch_bytes": (C.c_int, [_vp, _u64, _u64, C.POINTER(_u64)]),
     "srpc_gpu_pack_var": (C.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_unpack_var": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_fill_splitmix_i32": (C.c_int, [_vp, C.c_uint32, _u64, _u64, _u64, _vp]),

@@ -128,10 +128,13 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uin
     if (threadIdx.x == 0) partial[nb] = tot;
 }
 
-// out[i] = exclusive prefix of f over [0, i); out[n] = total.
+// out[i] = exclusive prefix of f over [0, i); out[n] = total.  With
+// tile_first, item i also records itself as the first item of every 4 KiB
+// output tile whose first byte it covers (start_i <= t*4096 < start_i + f(i)),
+// so a tile finds its first record with one load instead of a binary search.
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, uint64_t n, const uint64_t* partial, uint64_t nb,
-                                                       uint64_t* out) {
+                                                       uint64_t* out, uint64_t* tile_first, uint64_t max_tiles) {
     __shared__ uint64_t v[kScanBlock];
     const uint64_t base = blockIdx.x * kScanBlock;
 #pragma unroll
@@ -150,7 +153,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, uint64_t n, const ui
     uint64_t tot;
     const uint64_t pre = block_exclusive_scan(s, &tot) + partial[blockIdx.x];
 #pragma unroll
-    for (int j = 0; j < kScanItems; ++j) v[threadIdx.x * kScanItems + j] = pre + loc[j];
+    for (int j = 0; j < kScanItems; ++j) {
+        const uint32_t k = threadIdx.x * kScanItems + j;
+        const uint64_t start = pre + loc[j], end = start + v[k];
+        if (tile_first)
+            for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
+                tile_first[t] = base + k;
+        v[k] = start;
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kScanItems; ++j) {  // coalesced writes
@@ -174,18 +184,14 @@ __device__ __forceinline__ uint64_t upper_index(const uint64_t* offs, uint64_t n
     return lo;
 }
 
-// Per-tile helper: the tile's first covering record, then a window of the
-// following record starts in LDS.
+// Per-tile helper: a window of record starts from the tile's first covering
+// record r0 (tile_first, written by the scan) on, staged in LDS.
 struct Window {
     uint64_t r0;
     uint32_t len;  // entries valid in win[0..len)
 };
 
-__device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, uint64_t lo, uint64_t* win,
-                                              uint64_t* shared_r0) {
-    if (threadIdx.x == 0) *shared_r0 = upper_index(offs, n, lo);
-    __syncthreads();
-    const uint64_t r0 = *shared_r0;
+__device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, uint64_t r0, uint64_t* win) {
     const uint32_t len = static_cast<uint32_t>(min<uint64_t>(kWindow, n + 1 - r0));
     for (uint32_t k = threadIdx.x; k < len; k += kBlock) win[k] = offs[r0 + k];
     __syncthreads();
@@ -279,10 +285,10 @@ __device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* __restrict__ rec_offs, uint64_t n,
+                                                     const uint64_t* __restrict__ tile_first,
                                                      uint8_t* __restrict__ wire, uint64_t wire_cap,
                                                      srpc_unpack_status* st) {
     __shared__ uint64_t win[kWindow];
-    __shared__ uint64_t r0s;
     __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
     __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
     __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
-        const Window w = load_window(rec_offs, n, lo, win, &r0s);
+        const Window w = load_window(rec_offs, n, tile_first[t], win);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
@@ -390,16 +396,16 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
 // Chars of one string field: output chunk c = bytes [16c, 16c+16) of chars.
 __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                              const uint64_t* __restrict__ soff,
+                                                             const uint64_t* __restrict__ tile_first,
                                                              const uint64_t* __restrict__ spos, uint64_t n,
                                                              uint8_t* __restrict__ chars) {
     __shared__ uint64_t win[kWindow];
-    __shared__ uint64_t r0s;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
-        const Window w = load_window(soff, n, lo, win, &r0s);
+        const Window w = load_window(soff, n, tile_first[t], win);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < total) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
@@ -439,12 +445,14 @@ __global__ void k_reset_status(srpc_unpack_status* st) {
 uint64_t scan_blocks(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 
 template <class F>
-int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, hipStream_t s) {
+int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* tile_first, uint64_t max_tiles,
+                hipStream_t s) {
     const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
     if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial);
     hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb);
-    hipLaunchKernelGGL(k_scan_apply<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, nb, out);
+    hipLaunchKernelGGL(k_scan_apply<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, nb, out,
+                       tile_first, max_tiles);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
@@ -467,12 +475,27 @@ VarArgs make_var_args(const srpc_plan* p, const void* const* cols, const uint64_
     return a;
 }
 
-// scratch layout: [partials: nb+1 u64] ... (unpack) [lens: ns*n u64] [spos: ns*n u64]
-uint64_t scratch_need(const srpc_plan* p, uint64_t n, bool unpack) {
-    const uint64_t part = 8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1);
-    uint64_t b = (part + 255) & ~255ull;
-    if (unpack) b += 2 * 8 * static_cast<uint64_t>(p->nstrings) * n;
-    return b;
+// Scratch layout (each region 256-byte aligned):
+//   [partials: nb+1 u64] [tile_first: per tile domain, max_tiles u64]
+//   unpack only: [lens: ns*n u64] [spos: ns*n u64]
+// Pack has one tile domain (the wire); unpack one per string field (its chars).
+struct ScratchLayout {
+    uint64_t partial_off, tiles_off, lens_off, spos_off, total;
+    uint64_t max_tiles;
+};
+
+uint64_t round256(uint64_t b) { return (b + 255) & ~255ull; }
+
+ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes, bool unpack) {
+    ScratchLayout L{};
+    L.max_tiles = wire_bytes / kTileBytes + 1;
+    L.partial_off = 0;
+    L.tiles_off = round256(8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1));
+    const uint64_t domains = unpack ? p->nstrings : 1;
+    L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
+    L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
+    L.total = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
+    return L;
 }
 
 }  // namespace
@@ -482,13 +505,13 @@ using namespace srpc_impl;
 
 extern "C" {
 
-int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t* out) {
+int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_bytes, uint64_t* out) {
     if (!p || !out) return SRPC_E_INVALID;
     if (!p->has_string) {
         *out = 0;
         return SRPC_OK;
     }
-    *out = std::max(scratch_need(p, n, false), scratch_need(p, n, true));
+    *out = std::max(scratch_layout(p, n, wire_bytes, false).total, scratch_layout(p, n, wire_bytes, true).total);
     return SRPC_OK;
 }
 
@@ -502,18 +525,22 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
-    if (scratch_bytes < scratch_need(p, n, false)) return SRPC_E_CAPACITY;
+    const ScratchLayout L = scratch_layout(p, n, wire_cap, false);
+    if (scratch_bytes < L.total) return SRPC_E_CAPACITY;
     if (!aligned(wire, 16) || !aligned(rec_offs, 8) || !aligned(scratch, 8)) return SRPC_E_ALIGN;
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (!cols[f]) return SRPC_E_INVALID;
         if (p->size[f] == 0 && (!str_offs[f] || !aligned(str_offs[f], 8))) return SRPC_E_INVALID;
     }
     const VarArgs a = make_var_args(p, cols, str_offs);
-    int rc = launch_scan(PackSizes{a}, n, static_cast<uint64_t*>(scratch), rec_offs, s);
+    auto* base = static_cast<uint8_t*>(scratch);
+    auto* tiles = reinterpret_cast<uint64_t*>(base + L.tiles_off);
+    int rc = launch_scan(PackSizes{a}, n, reinterpret_cast<uint64_t*>(base + L.partial_off), rec_offs, tiles,
+                         L.max_tiles, s);
     if (rc) return rc;
     if (n == 0) return SRPC_OK;
     if (!wire) return SRPC_E_INVALID;
-    hipLaunchKernelGGL(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, wire, wire_cap, st);
+    hipLaunchKernelGGL(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
@@ -527,7 +554,8 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
-    if (scratch_bytes < scratch_need(p, n, true)) return SRPC_E_CAPACITY;
+    const ScratchLayout L = scratch_layout(p, n, wire_len, true);
+    if (scratch_bytes < L.total) return SRPC_E_CAPACITY;
     if (!aligned(scratch, 8) || !aligned(rec_offs, 8)) return SRPC_E_ALIGN;
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (!cols[f]) return SRPC_E_INVALID;
@@ -537,10 +565,11 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     }
     const VarArgs a = make_var_args(p, reinterpret_cast<const void* const*>(cols),
                                     reinterpret_cast<const uint64_t* const*>(str_offs));
-    auto* partial = static_cast<uint64_t*>(scratch);
-    const uint64_t part = 8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1);
-    auto* lens = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) + ((part + 255) & ~255ull));
-    uint64_t* spos = lens + static_cast<uint64_t>(p->nstrings) * n;
+    auto* base = static_cast<uint8_t*>(scratch);
+    auto* partial = reinterpret_cast<uint64_t*>(base + L.partial_off);
+    auto* tiles = reinterpret_cast<uint64_t*>(base + L.tiles_off);
+    auto* lens = reinterpret_cast<uint64_t*>(base + L.lens_off);
+    auto* spos = reinterpret_cast<uint64_t*>(base + L.spos_off);
     const uint64_t grid = (n + kBlock - 1) / kBlock;
     if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     if (n) {
@@ -550,13 +579,15 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     }
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
-        int rc = launch_scan(ArrayVals{lens + a.sidx[f] * n}, n, partial, str_offs[f], s);
+        int rc = launch_scan(ArrayVals{lens + a.sidx[f] * n}, n, partial, str_offs[f],
+                             tiles + a.sidx[f] * L.max_tiles, L.max_tiles, s);
         if (rc) return rc;
     }
     if (n == 0) return SRPC_OK;
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
         hipLaunchKernelGGL(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
+                           tiles + a.sidx[f] * L.max_tiles,
                            spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;

@@ -166,9 +166,10 @@ class GpuPacker:
                      "srpc_gpu_unpack")
 
     # -- string schemas (SRPC_PATH_VAR) -------------------------------------
-    def var_scratch_bytes(self, n: int) -> int:
+    def var_scratch_bytes(self, n: int, wire_bytes: int) -> int:
+        """Device scratch for pack_var (wire_bytes = wire_cap) / unpack_var (= wire_len)."""
         out = C.c_uint64()
-        check(_lib.lib().srpc_plan_var_scratch_bytes(self._h, n, C.byref(out)),
+        check(_lib.lib().srpc_plan_var_scratch_bytes(self._h, n, wire_bytes, C.byref(out)),
               "srpc_plan_var_scratch_bytes")
         return out.value
 

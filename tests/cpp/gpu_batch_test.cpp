@@ -140,7 +140,7 @@ static int run_var(srpc::gpu::batch_packer<Text>& bp, size_t n, std::mt19937_64&
     uint8_t* dw = nullptr;
     uint64_t* drec = nullptr;
     void* scratch = nullptr;
-    const uint64_t sb = bp.scratch_bytes(n);
+    const uint64_t sb = bp.scratch_bytes(n, want.size());
     HIPCHECK(hipMalloc(&dw, want.size() + 16));
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&drec), 8 * (n + 1)));
     HIPCHECK(hipMalloc(&scratch, sb + 16));

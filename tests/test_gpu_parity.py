@@ -320,7 +320,7 @@ def gpu_pack_var(p, kinds, cols, offs, n):
         len(p.prefix) + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds))
     wire = empty(total + 16)
     rec = empty(8 * (n + 1))
-    sb = p.var_scratch_bytes(n)
+    sb = p.var_scratch_bytes(n, total)
     scratch = empty(sb + 16)
     st = status_buf()
     p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, st)
@@ -339,7 +339,7 @@ def gpu_unpack_var(p, kinds, wire: bytes, n, rec_offs, wire_len=None):
         else:
             outs.append(empty(n * oracle.KIND_SIZE[k] + 16))
             offs.append(None)
-    sb = p.var_scratch_bytes(n)
+    sb = p.var_scratch_bytes(n, L)
     scratch = empty(sb + 16)
     st = status_buf()
     p.unpack_var(w, L, n, _dev_u64(rec_offs), outs, offs, scratch, sb, st)
@@ -468,10 +468,10 @@ def test_strings_errors():
     dcols = [dev(c) for c in cols]
     doffs = [None, _dev_u64(offs[1])]
     recd = empty(8 * (n + 1))
-    sb = p.var_scratch_bytes(n)
+    small = int(rec[600]) + 3
+    sb = p.var_scratch_bytes(n, small)
     scratch = empty(sb + 16)
     s = status_buf()
-    small = int(rec[600]) + 3
     w = empty(int(rec[n]) + 16)
     p.pack_var(dcols, doffs, n, w, small, recd, scratch, sb, s)
     assert read_status(s) == (srpc_amd.SRPC_STATUS_BOUNDS, 600)

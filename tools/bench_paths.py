@@ -111,7 +111,7 @@ def main():
         doffs = [t_u8(o) if o is not None else None for o in offs]
         wire = torch.empty(total + 16, dtype=torch.uint8, device=dev)
         rec = torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev)
-        sb = p.var_scratch_bytes(n)
+        sb = p.var_scratch_bytes(n, total)
         scratch = torch.empty(sb + 16, dtype=torch.uint8, device=dev)
         outs = [torch.empty(total + 16 if k == oracle.STRING else n * oracle.KIND_SIZE[k] + 16,
                             dtype=torch.uint8, device=dev) for k in kinds]
