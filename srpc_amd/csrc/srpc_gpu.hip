@@ -231,6 +231,9 @@ __global__ __launch_bounds__(kBlock) void k_unpack_dword_x4(DwordMap m, const ui
 // ---------------------------------------------------------------------------
 // TILE path
 // ---------------------------------------------------------------------------
+// Independent 16-byte global loads each lane issues before using any of them.
+constexpr int kLoadBatch = 8;
+
 // LDS layout (dynamic, 16-byte aligned base): image[R*stride] | tmpl[L] | mask[L]
 __device__ __forceinline__ void build_template(const TileArgs& a, uint8_t* tmpl, uint8_t* mask) {
     for (uint32_t i = threadIdx.x; i < a.L; i += kBlock) {
@@ -284,22 +287,30 @@ __global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __res
             const uint8_t* src = a.col[f] + rbase * s;
             const uint32_t nbytes = nr * s;
             const uint32_t nchunks = (nbytes + 15) >> 4;
-            for (uint32_t c = threadIdx.x; c < nchunks; c += kBlock) {
-                uint4 q;
-                if ((c + 1) * 16 <= nbytes) {
-                    q = *reinterpret_cast<const uint4*>(src + 16 * c);
-                } else {
-                    q = make_uint4(0, 0, 0, 0);
-                    uint8_t* qb = reinterpret_cast<uint8_t*>(&q);
-                    for (uint32_t i = 16 * c; i < nbytes; ++i) qb[i - 16 * c] = src[i];
+            for (uint32_t c0 = threadIdx.x; c0 < nchunks; c0 += kBlock * kLoadBatch) {
+                uint4 qq[kLoadBatch];
+#pragma unroll
+                for (int u = 0; u < kLoadBatch; ++u) {
+                    const uint32_t c = c0 + u * kBlock;
+                    if ((c + 1) * 16 <= nbytes) qq[u] = *reinterpret_cast<const uint4*>(src + 16 * c);
                 }
-                const uint32_t e0 = (16 * c) >> lg;
-                const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
-                switch (s) {
-                case 1: scatter_chunk<1>(img, q, e0, ne, a.stride, a.off[f]); break;
-                case 2: scatter_chunk<2>(img, q, e0, ne, a.stride, a.off[f]); break;
-                case 4: scatter_chunk<4>(img, q, e0, ne, a.stride, a.off[f]); break;
-                default: scatter_chunk<8>(img, q, e0, ne, a.stride, a.off[f]); break;
+#pragma unroll
+                for (int u = 0; u < kLoadBatch; ++u) {
+                    const uint32_t c = c0 + u * kBlock;
+                    if (c >= nchunks) break;
+                    const uint32_t e0 = (16 * c) >> lg;
+                    const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+                    if ((c + 1) * 16 > nbytes) {  // the column's last, partial chunk: whole elements, bytewise
+                        for (uint32_t e = e0; e < nr; ++e)
+                            for (uint32_t i = 0; i < s; ++i) img[e * a.stride + a.off[f] + i] = src[e * s + i];
+                        continue;
+                    }
+                    switch (s) {
+                    case 1: scatter_chunk<1>(img, qq[u], e0, ne, a.stride, a.off[f]); break;
+                    case 2: scatter_chunk<2>(img, qq[u], e0, ne, a.stride, a.off[f]); break;
+                    case 4: scatter_chunk<4>(img, qq[u], e0, ne, a.stride, a.off[f]); break;
+                    default: scatter_chunk<8>(img, qq[u], e0, ne, a.stride, a.off[f]); break;
+                    }
                 }
             }
         }
@@ -345,22 +356,35 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
         const uint8_t* src = wire + rbase * a.stride;
         const uint32_t tbytes = nr * a.stride;
         const uint32_t full = tbytes >> 4;
-        for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
-            const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * c);
-            if (a.prefix_len && st) {
-                const uint32_t ph = (16 * c) % a.L;
-                const uint4 m = *reinterpret_cast<const uint4*>(mask + ph);
-                const uint4 t = *reinterpret_cast<const uint4*>(tmpl + ph);
-                if (((v.x & m.x) != t.x) | ((v.y & m.y) != t.y) | ((v.z & m.z) != t.z) |
-                    ((v.w & m.w) != t.w)) {
-                    // first record touched by a differing byte of this chunk
-                    uint32_t i = 16 * c;
-                    const uint8_t* vb = reinterpret_cast<const uint8_t*>(&v);
-                    while ((vb[i - 16 * c] & mask[(i) % a.L]) == tmpl[(i) % a.L]) ++i;
-                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
-                }
+        // kLoadBatch independent 16-byte loads in flight per lane before any is used
+        for (uint32_t c0 = threadIdx.x; c0 < full; c0 += kBlock * kLoadBatch) {
+            uint4 vv[kLoadBatch];
+#pragma unroll
+            for (int u = 0; u < kLoadBatch; ++u) {
+                const uint32_t c = c0 + u * kBlock;
+                if (c < full) vv[u] = *reinterpret_cast<const uint4*>(src + 16 * c);
             }
-            *reinterpret_cast<uint4*>(img + 16 * c) = v;
+#pragma unroll
+            for (int u = 0; u < kLoadBatch; ++u) {
+                const uint32_t c = c0 + u * kBlock;
+                if (c >= full) break;
+                const uint4 v = vv[u];
+                if (a.prefix_len && st) {
+                    const uint32_t ph = (16 * c) % a.L;
+                    const uint4 m = *reinterpret_cast<const uint4*>(mask + ph);
+                    const uint4 t = *reinterpret_cast<const uint4*>(tmpl + ph);
+                    const uint32_t d0 = (v.x & m.x) ^ t.x, d1 = (v.y & m.y) ^ t.y;
+                    const uint32_t d2 = (v.z & m.z) ^ t.z, d3 = (v.w & m.w) ^ t.w;
+                    if (d0 | d1 | d2 | d3) {
+                        // first record touched by a differing byte of this chunk
+                        const uint32_t w = d0 ? 0 : d1 ? 1 : d2 ? 2 : 3;
+                        const uint32_t dw = d0 ? d0 : d1 ? d1 : d2 ? d2 : d3;
+                        const uint32_t i = 16 * c + 4 * w + (__builtin_ctz(dw) >> 3);
+                        report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                    }
+                }
+                *reinterpret_cast<uint4*>(img + 16 * c) = v;
+            }
         }
         if (threadIdx.x == 0) {
             for (uint32_t i = full * 16; i < tbytes; ++i) {
@@ -390,9 +414,9 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
                 }
                 if ((c + 1) * 16 <= nbytes) {
                     *reinterpret_cast<uint4*>(dstc + 16 * c) = q;
-                } else {
-                    const uint8_t* qb = reinterpret_cast<const uint8_t*>(&q);
-                    for (uint32_t i = 16 * c; i < nbytes; ++i) dstc[i] = qb[i - 16 * c];
+                } else {  // the column's last, partial chunk: whole elements, bytewise from the image
+                    for (uint32_t e = e0; e < nr; ++e)
+                        for (uint32_t i = 0; i < s; ++i) dstc[e * s + i] = img[e * a.stride + a.off[f] + i];
                 }
             }
         }
@@ -694,9 +718,9 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         }
     }
     if (p->dword_ok) p->dv = default_dword_variant(static_cast<uint32_t>(o / 4));
-    // TILE image size: the best of 4-48 KiB per record width on MI355X
-    // (profiles/r01_sweep_tile.log): 16 KiB for narrow records, 32 KiB for wide.
-    if (o <= kMaxTileStride) configure_tile(p, o >= 32 ? 32768 : 16384);
+    // TILE image size: 32 KiB, the best or within 3 % of the best of 4-48 KiB
+    // for every record width swept on MI355X (profiles/r01_sweep_tile.log).
+    if (o <= kMaxTileStride) configure_tile(p, 32768);
     *out = p;
     return SRPC_OK;
 }
