@@ -30,6 +30,7 @@ struct DwordVariant {
     int rpl = 1;
     int iter = 1;
     int nt = kNtStore | kNtLoad;
+    int grid = 0;  // 0: one workgroup per 256*iter records; >0: at most this many (grid-stride)
 };
 
 __device__ __forceinline__ void report_bad(srpc_unpack_status* st, uint32_t flag, uint64_t rec) {

@@ -126,39 +126,43 @@ __device__ __forceinline__ void load_record(const uint8_t* p, uint32_t (&v)[W]) 
 template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_pack_dword(DwordMap m, uint8_t* __restrict__ wire,
                                                        uint64_t n) {
-    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
-    uint32_t v[ITER][W];
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * (kBlock * ITER);
+    for (uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x; r0 < n; r0 += step) {
+        uint32_t v[ITER][W];
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) {
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+            if (r < n) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) v[it][k] = ld<NT>(m.src[k] + (r << m.lg[k]));
+                for (int k = 0; k < W; ++k) v[it][k] = ld<NT>(m.src[k] + (r << m.lg[k]));
+            }
         }
-    }
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) store_record<W, NT>(wire + r * (4 * W), v[it]);
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+            if (r < n) store_record<W, NT>(wire + r * (4 * W), v[it]);
+        }
     }
 }
 
 template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_unpack_dword(DwordMap m, const uint8_t* __restrict__ wire,
                                                          uint64_t n) {
-    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
-    uint32_t v[ITER][W];
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * (kBlock * ITER);
+    for (uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x; r0 < n; r0 += step) {
+        uint32_t v[ITER][W];
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) load_record<W, NT>(wire + r * (4 * W), v[it]);
-    }
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+            if (r < n) load_record<W, NT>(wire + r * (4 * W), v[it]);
+        }
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
-        if (r < n) {
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t r = r0 + static_cast<uint64_t>(it) * kBlock;
+            if (r < n) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) st<NT>(const_cast<uint32_t*>(m.src[k]) + (r << m.lg[k]), v[it][k]);
+                for (int k = 0; k < W; ++k) st<NT>(const_cast<uint32_t*>(m.src[k]) + (r << m.lg[k]), v[it][k]);
+            }
         }
     }
 }
@@ -170,29 +174,31 @@ __global__ __launch_bounds__(kBlock) void k_unpack_dword(DwordMap m, const uint8
 template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_pack_dword_x4(DwordMap m, uint8_t* __restrict__ wire,
                                                           uint64_t nq) {
-    const uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
-    u32x4 c[ITER][W];
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * (kBlock * ITER);
+    for (uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x; q0 < nq; q0 += step) {
+        u32x4 c[ITER][W];
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
-        if (q < nq) {
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+            if (q < nq) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) c[it][k] = ld<NT>(reinterpret_cast<const u32x4*>(m.src[k]) + q);
+                for (int k = 0; k < W; ++k) c[it][k] = ld<NT>(reinterpret_cast<const u32x4*>(m.src[k]) + q);
+            }
         }
-    }
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
-        if (q < nq) {
-            uint32_t o[4 * W];
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+            if (q < nq) {
+                uint32_t o[4 * W];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int k = 0; k < W; ++k) o[i * W + k] = c[it][k][i];
-            u32x4* dst = reinterpret_cast<u32x4*>(wire + q * (16 * W));
+                    for (int k = 0; k < W; ++k) o[i * W + k] = c[it][k][i];
+                u32x4* dst = reinterpret_cast<u32x4*>(wire + q * (16 * W));
 #pragma unroll
-            for (int j = 0; j < W; ++j)
-                st<NT>(dst + j, u32x4{o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]});
+                for (int j = 0; j < W; ++j)
+                    st<NT>(dst + j, u32x4{o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]});
+            }
         }
     }
 }
@@ -200,30 +206,32 @@ __global__ __launch_bounds__(kBlock) void k_pack_dword_x4(DwordMap m, uint8_t* _
 template <int W, int ITER, int NT>
 __global__ __launch_bounds__(kBlock) void k_unpack_dword_x4(DwordMap m, const uint8_t* __restrict__ wire,
                                                             uint64_t nq) {
-    const uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x;
-    u32x4 c[ITER][W];
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * (kBlock * ITER);
+    for (uint64_t q0 = static_cast<uint64_t>(blockIdx.x) * (kBlock * ITER) + threadIdx.x; q0 < nq; q0 += step) {
+        u32x4 c[ITER][W];
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
-        if (q < nq) {
-            const u32x4* src = reinterpret_cast<const u32x4*>(wire + q * (16 * W));
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+            if (q < nq) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(wire + q * (16 * W));
 #pragma unroll
-            for (int j = 0; j < W; ++j) c[it][j] = ld<NT>(src + j);
+                for (int j = 0; j < W; ++j) c[it][j] = ld<NT>(src + j);
+            }
         }
-    }
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
-        if (q < nq) {
-            uint32_t o[4 * W];
+        for (int it = 0; it < ITER; ++it) {
+            const uint64_t q = q0 + static_cast<uint64_t>(it) * kBlock;
+            if (q < nq) {
+                uint32_t o[4 * W];
 #pragma unroll
-            for (int j = 0; j < W; ++j)
+                for (int j = 0; j < W; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[4 * j + e] = c[it][j][e];
+                    for (int e = 0; e < 4; ++e) o[4 * j + e] = c[it][j][e];
 #pragma unroll
-            for (int k = 0; k < W; ++k)
-                st<NT>(reinterpret_cast<u32x4*>(const_cast<uint32_t*>(m.src[k])) + q,
-                       u32x4{o[k], o[W + k], o[2 * W + k], o[3 * W + k]});
+                for (int k = 0; k < W; ++k)
+                    st<NT>(reinterpret_cast<u32x4*>(const_cast<uint32_t*>(m.src[k])) + q,
+                           u32x4{o[k], o[W + k], o[2 * W + k], o[3 * W + k]});
+            }
         }
     }
 }
@@ -469,13 +477,15 @@ namespace {
 using namespace srpc_impl;
 
 template <int W, int ITER, int NT>
-int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, hipStream_t s) {
+int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, int max_grid, hipStream_t s) {
     const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
+    // kernels are grid-stride: max_grid > 0 caps the workgroup count
+    auto cap = [max_grid](uint64_t g) { return max_grid > 0 ? std::min<uint64_t>(g, max_grid) : g; };
     uint64_t done = 0;
     if (rpl == 4) {
         const uint64_t nq = n / 4;
         if (nq) {
-            const uint64_t grid = (nq + per - 1) / per;
+            const uint64_t grid = cap((nq + per - 1) / per);
             if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
             if (pack)
                 hipLaunchKernelGGL((k_pack_dword_x4<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)),
@@ -491,7 +501,7 @@ int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int 
         DwordMap t = m;
         for (int k = 0; k < W; ++k) t.src[k] += done << t.lg[k];
         const uint64_t rest = n - done;
-        const uint64_t grid = (rest + per - 1) / per;
+        const uint64_t grid = cap((rest + per - 1) / per);
         if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
         if (pack)
             hipLaunchKernelGGL((k_pack_dword<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
@@ -512,10 +522,10 @@ int launch_dword(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, const 
     if constexpr (W == 1 || W == 2 || W == 4) {
 #define SRPC_NT_CASES(IT)                                                        \
     switch (v.nt) {                                                              \
-    case 0: return launch_dword_v<W, IT, 0>(pack, m, wire, n, v.rpl, s);         \
-    case 1: return launch_dword_v<W, IT, 1>(pack, m, wire, n, v.rpl, s);         \
-    case 2: return launch_dword_v<W, IT, 2>(pack, m, wire, n, v.rpl, s);         \
-    default: return launch_dword_v<W, IT, 3>(pack, m, wire, n, v.rpl, s);        \
+    case 0: return launch_dword_v<W, IT, 0>(pack, m, wire, n, v.rpl, v.grid, s);         \
+    case 1: return launch_dword_v<W, IT, 1>(pack, m, wire, n, v.rpl, v.grid, s);         \
+    case 2: return launch_dword_v<W, IT, 2>(pack, m, wire, n, v.rpl, v.grid, s);         \
+    default: return launch_dword_v<W, IT, 3>(pack, m, wire, n, v.rpl, v.grid, s);        \
     }
         switch (v.iter) {
         case 1: SRPC_NT_CASES(1)
@@ -525,7 +535,7 @@ int launch_dword(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, const 
         }
 #undef SRPC_NT_CASES
     } else {
-        return launch_dword_v<W, 4, 0>(pack, m, wire, n, 1, s);
+        return launch_dword_v<W, 4, 0>(pack, m, wire, n, 1, v.grid, s);
     }
 }
 
@@ -774,6 +784,10 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
     case SRPC_TUNE_NONTEMPORAL:
         if (value < 0 || value > 3) return SRPC_E_INVALID;
         p->dv.nt = value;
+        return SRPC_OK;
+    case SRPC_TUNE_GRID:
+        if (value < 0) return SRPC_E_INVALID;
+        p->dv.grid = value;
         return SRPC_OK;
     case SRPC_TUNE_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;

@@ -131,10 +131,12 @@ class GpuPacker:
         check(_lib.lib().srpc_plan_force_path(self._h, path), "srpc_plan_force_path")
 
     def tune(self, records_per_lane: int | None = None, iters: int | None = None,
-             nontemporal: int | None = None, tile_bytes: int | None = None) -> None:
+             nontemporal: int | None = None, tile_bytes: int | None = None,
+             grid: int | None = None) -> None:
         """Performance knobs (srpc_plan_tune); output bytes never change."""
         L = _lib.lib()
-        for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal), (4, tile_bytes)):
+        for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal), (4, tile_bytes),
+                          (5, grid)):
             if val is not None:
                 check(L.srpc_plan_tune(self._h, knob, int(val)), "srpc_plan_tune")
 

@@ -178,13 +178,13 @@ def test_dword_variants_identical(schema):
             .view(oracle.KIND_DTYPE[k]) for k in kinds]
     want = oracle.pack(kinds, cols, n)
     p = GpuPacker(sch)
-    for rpl in (1, 4):
-        for it in (1, 2, 4, 8):
-            for nt in range(4):
-                p.tune(rpl, it, nt)
-                assert gpu_pack(p, cols, n) == want, (rpl, it, nt)
-                rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
-                assert rc == 0 and all(a.tobytes() == b.tobytes() for a, b in zip(cols, back)), (rpl, it, nt)
+    variants = [(r, i, t, 0) for r in (1, 4) for i in (1, 2, 4, 8) for t in range(4)]
+    variants += [(1, 1, 3, 7), (4, 2, 0, 3), (1, 4, 2, 1)]  # capped grids: grid-stride loops
+    for rpl, it, nt, grid in variants:
+        p.tune(rpl, it, nt, grid=grid)
+        assert gpu_pack(p, cols, n) == want, (rpl, it, nt, grid)
+        rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+        assert rc == 0 and all(a.tobytes() == b.tobytes() for a, b in zip(cols, back)), (rpl, it, nt, grid)
 
 
 # ---- envelopes (Calculator.square) ---------------------------------------------

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--schema", default="quad", choices=["quad", "number", "two"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--grids", default="", help="comma list of workgroup caps to sweep (0 = full grid)")
+    ap.add_argument("--base", default="1,1,3", help="rpl,iter,nt for the --grids sweep")
     args = ap.parse_args()
 
     import torch
@@ -53,8 +55,13 @@ def main():
     copy_dst = torch.empty_like(copy_src)
     p = GpuPacker(sch)
 
-    variants = [("dword", rpl, it, nt) for rpl, it, nt in itertools.product((1, 4), (1, 2, 4, 8), (0, 1, 2, 3))]
-    variants.append(("tile", 0, 0, 0))
+    if args.grids:
+        base = [int(x) for x in args.base.split(",")]
+        variants = [("dword", base[0], base[1], base[2], g) for g in [int(x) for x in args.grids.split(",")]]
+    else:
+        variants = [("dword", rpl, it, nt, 0)
+                    for rpl, it, nt in itertools.product((1, 4), (1, 2, 4, 8), (0, 1, 2, 3))]
+        variants.append(("tile", 0, 0, 0, 0))
     alg = 2 * 4 * F * n  # bytes per kernel: read F*4 + write F*4 per record
 
     def timed(fn, cold):
@@ -110,7 +117,7 @@ def set_variant(p, v, srpc_amd):
         p.force_path(srpc_amd.SRPC_PATH_TILE)
     else:
         p.force_path(srpc_amd.SRPC_PATH_DWORD)
-        p.tune(v[1], v[2], v[3])
+        p.tune(v[1], v[2], v[3], grid=v[4])
 
 
 if __name__ == "__main__":
