@@ -41,7 +41,7 @@ namespace {
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 2048 items
 constexpr uint32_t kTileBytes = kBlock * 16;                                  // 4 KiB output tile
-constexpr uint32_t kWindow = 1024;  // record starts staged in LDS per tile
+constexpr uint32_t kWindow = 528;   // record starts staged in LDS per tile (>= 4096/8 + 2)
 constexpr int kVarGrid = 2048;      // resident workgroups for grid-stride tiles
 
 struct VarArgs {
@@ -198,6 +198,18 @@ __device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, 
     return {r0, len};
 }
 
+// The window plus the same records' entries of a second offsets array.
+__device__ __forceinline__ Window load_window2(const uint64_t* offs, const uint64_t* offs2, uint64_t n, uint64_t r0,
+                                               uint64_t* win, uint64_t* win2) {
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(kWindow, n + 1 - r0));
+    for (uint32_t k = threadIdx.x; k < len; k += kBlock) {
+        win[k] = offs[r0 + k];
+        win2[k] = offs2[r0 + k];
+    }
+    __syncthreads();
+    return {r0, len};
+}
+
 // Covering record of byte p using the window (global search when p lies past it).
 __device__ __forceinline__ uint64_t find_record(const uint64_t* offs, uint64_t n, const Window& w,
                                                 const uint64_t* win, uint64_t p) {
@@ -241,8 +253,10 @@ __device__ __forceinline__ T load_unaligned(const uint8_t* p) {
 // Write `cnt` (<= 16) bytes of record r, from byte q of the record, to dst
 // (an LDS slot with 16 bytes of slack after dst).  Segments in wire order:
 // prefix, then every field (fixed value | u64 length, chars).
+// sw (may be null): LDS copy of soff[f0][r], soff[f0][r+1] for the first string field f0.
 __device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_t* pre, const uint64_t* climit,
-                                                  uint64_t n, uint64_t r, uint64_t q, uint32_t cnt, uint8_t* dst) {
+                                                  uint32_t f0, const uint64_t* sw, uint64_t n, uint64_t r, uint64_t q,
+                                                  uint32_t cnt, uint8_t* dst) {
     const uint64_t end = q + cnt;
     if (q < a.prefix_len) {
         const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, a.prefix_len) - q);
@@ -264,7 +278,9 @@ __device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_
             }
             s += sz;
         } else {
-            const uint64_t b0 = a.soff[f][r], len = a.soff[f][r + 1] - b0;
+            const bool staged = f == f0 && sw;
+            const uint64_t b0 = staged ? sw[0] : a.soff[f][r];
+            const uint64_t len = (staged ? sw[1] : a.soff[f][r + 1]) - b0;
             if (q < s + 8) {
                 const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + 8) - q);
                 const uint64_t v = len >> (8 * (q - s));
@@ -289,7 +305,10 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
                                                      uint8_t* __restrict__ wire, uint64_t wire_cap,
                                                      srpc_unpack_status* st) {
     __shared__ uint64_t win[kWindow];
+    __shared__ uint64_t swin[kWindow];       // char offsets of the first string field, same records
     __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
+    uint32_t f0 = 0;                         // the first string field
+    while (a.size[f0]) ++f0;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
     __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
     for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
@@ -301,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
-        const Window w = load_window(rec_offs, n, tile_first[t], win);
+        const Window w = load_window2(rec_offs, a.soff[f0], n, tile_first[t], win, swin);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
@@ -314,7 +333,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
                 const uint64_t rs = k + 1 < w.len ? win[k] : rec_offs[r];
                 const uint64_t re = k + 1 < w.len ? win[k + 1] : rec_offs[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                emit_record_bytes(a, pre, climit, n, r, p - rs, cnt, slot + b);
+                emit_record_bytes(a, pre, climit, f0, k + 1 < w.len ? swin + k : nullptr, n, r, p - rs, cnt,
+                                  slot + b);
                 b += cnt;
                 p += cnt;
                 ++r;
