@@ -40,8 +40,8 @@ ALG_BYTES_PER_REC = 32          # per kernel: pack reads 4x4 B + writes 16 B; un
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--records", type=int, default=1 << 24, help="records per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline work (rank 0, N=1 only); 0 disables")
@@ -173,6 +173,13 @@ def main() -> None:
             verify["roundtrip"] = bool(flag.item())
         del full
 
+    K = args.steps
+    step0 = torch.cuda.Event(enable_timing=True)
+    step1 = torch.cuda.Event(enable_timing=True)
+    kev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    for e in [step0, step1] + [e for row in kev for e in row]:
+        e.record(stream)  # torch creates the HIP event on its first record
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -180,24 +187,33 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    K = args.steps
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    # Step clock (`value`, ms_per_step): K uninstrumented steps.
     t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record(stream)
-        p.pack(cols, n, wire, stream=stream)
-        ev[i][1].record(stream)
-        p.unpack(wire, n * REC_BYTES, n, back, stream=stream)
-        ev[i][2].record(stream)
+    step0.record(stream)
+    for _ in range(K):
+        step()
+    step1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
 
-    pack_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(K)]
-    unpack_ms = [ev[i][1].elapsed_time(ev[i][2]) for i in range(K)]
-    gpu_ms = ev[0][0].elapsed_time(ev[K - 1][2])
+    # Kernel clock (roofline): K further steps with every pack / unpack call
+    # armed by srpc_time_next_call, so its kernel stamps its own dispatch
+    # begin/end into a per-call event pair -- the interval rocprofv3
+    # --kernel-trace reports.  Arming costs ~5 us of GPU time per call
+    # (profiles/r01_step_overhead.json), so it stays out of the step clock.
+    for i in range(K):
+        srpc_amd.time_next_call(kev[i][0], kev[i][1])
+        p.pack(cols, n, wire, stream=stream)
+        srpc_amd.time_next_call(kev[i][2], kev[i][3])
+        p.unpack(wire, n * REC_BYTES, n, back, stream=stream)
+    torch.cuda.synchronize(dev)
+
+    pack_ms = [kev[i][0].elapsed_time(kev[i][1]) for i in range(K)]
+    unpack_ms = [kev[i][2].elapsed_time(kev[i][3]) for i in range(K)]
+    gpu_ms = step0.elapsed_time(step1)
     t_rank = max(elapsed, gpu_ms / 1e3)
     t = torch.tensor([t_rank, sum(pack_ms) / K, sum(unpack_ms) / K], dtype=torch.float64,
                      device=dev if args.dist_backend == "nccl" else "cpu")
@@ -255,7 +271,7 @@ def main() -> None:
         value = total_recs * K * REC_BYTES / 2**30 / t_max  # wire GiB/s, all ranks
         dom_name, dom_ms = ("pack", pack_avg) if pack_avg >= unpack_avg else ("unpack", unpack_avg)
         achieved = ALG_BYTES_PER_REC * n / (dom_ms / 1e3) / 1e9
-        traffic = None
+        traffic = rocprof_us = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
             with open(prof) as f:
@@ -263,6 +279,7 @@ def main() -> None:
             ent = pm.get("kernels", {}).get(dom_name)
             if ent and pm.get("records") == n:
                 traffic = ent.get("hbm_bytes_per_launch")
+                rocprof_us = round(ent["avg_ns"] / 1e3, 2) if ent.get("avg_ns") else None
         line = {
             "metric": "packer GiB/s + Mrecords/s device-resident, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -283,13 +300,15 @@ def main() -> None:
                        "tune": args.tune or "default"},
             "mrecords_per_s": round(total_recs * K / t_max / 1e6, 1),
             "hbm_algorithmic_GBps": round(2 * ALG_BYTES_PER_REC * total_recs * K / t_max / 1e9, 1),
-            "kernels_ms": {"pack": round(pack_avg, 4), "unpack": round(unpack_avg, 4)},
+            "kernels_ms": {"pack": round(pack_avg, 4), "unpack": round(unpack_avg, 4),
+                           "clock": "dispatch begin/end stamped by hipExtLaunchKernel (srpc_time_next_call), K armed steps after the step clock"},
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "frac_of_measured_copy": round(achieved / HBM_MEASURED_COPY_GBPS, 4),
                          "alg_bytes_per_launch": ALG_BYTES_PER_REC * n,
-                         "traffic": traffic},
+                         "traffic": traffic,
+                         "committed_rocprof_avg_us": rocprof_us},
             "verify": verify,
         }
         if gather:

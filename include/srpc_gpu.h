@@ -189,6 +189,16 @@ int srpc_gpu_unpack_var(const srpc_plan* plan, const uint8_t* d_wire, uint64_t w
 int srpc_gpu_fill_splitmix_i32(int32_t* const* d_cols, uint32_t nfields, uint64_t n,
                                uint64_t seed, uint64_t first_record, void* stream);
 
+/* Measurement hook (bench.py): the data-path kernels launched by the NEXT
+ * srpc_gpu_pack / _unpack / _pack_var / _unpack_var call made on this host
+ * thread record the begin timestamp of the first kernel into `start_event`
+ * and the end timestamp of the last into `stop_event` (hipEvent_t handles
+ * created with timing enabled; either may be NULL), taken from the dispatch
+ * packets themselves (hipExtLaunchKernel) -- kernel-only time, the interval
+ * rocprofv3 --kernel-trace reports.  Status-reset launches are not timed.
+ * The hook is consumed by that one call, whatever it returns. */
+int srpc_time_next_call(void* start_event, void* stop_event);
+
 const char* srpc_status_string(int code);
 int srpc_gpu_abi_version(void);
 

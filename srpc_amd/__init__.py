@@ -6,7 +6,7 @@ tests and ``bench.py``.  C++ callers use ``include/srpc/gpu.hpp`` instead.
 """
 from .packer import (BOOL, CHAR, INT8, INT16, INT32, INT64, RPC_ERR_FUNCTION_NOT_REGISTERED,
                      RPC_ERR_RECV_TIMEOUT, RPC_SUCCESS, STRING, GpuPacker, Schema, SrpcError,
-                     fill_splitmix_i32, request_prefix, response_prefix)
+                     fill_splitmix_i32, request_prefix, response_prefix, time_next_call)
 from ._lib import (SRPC_ERR_BOUNDS, SRPC_PATH_DWORD, SRPC_PATH_TILE, SRPC_PATH_VAR, SRPC_STATUS_BOUNDS,
                    SRPC_STATUS_PREFIX, UnpackStatus)
 
@@ -16,7 +16,7 @@ TWO_NUMBERS = Schema.of("TwoNumbers", ("left", "int32"), ("right", "int32"))  # 
 QUAD = Schema.of("Quad", ("a", "int32"), ("b", "int32"), ("c", "int32"), ("d", "int32"))
 SQUARE_METHOD = "Calculator_servicer::square"  # generator.hpp:84 naming, calculator_srpc.cpp:123
 
-__all__ = ["GpuPacker", "Schema", "SrpcError", "fill_splitmix_i32", "request_prefix",
+__all__ = ["GpuPacker", "Schema", "SrpcError", "fill_splitmix_i32", "time_next_call", "request_prefix",
            "response_prefix", "NUMBER", "TWO_NUMBERS", "QUAD", "SQUARE_METHOD", "BOOL", "INT8",
            "CHAR", "INT16", "INT32", "INT64", "STRING", "RPC_SUCCESS",
            "RPC_ERR_FUNCTION_NOT_REGISTERED", "RPC_ERR_RECV_TIMEOUT", "SRPC_ERR_BOUNDS",

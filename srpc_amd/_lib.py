@@ -44,6 +44,7 @@ SIGNATURES = {
     "srpc_gpu_pack_var": (C.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_unpack_var": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_fill_splitmix_i32": (C.c_int, [_vp, C.c_uint32, _u64, _u64, _u64, _vp]),
+    "srpc_time_next_call": (C.c_int, [_vp, _vp]),
     "srpc_status_string": (C.c_char_p, [C.c_int]),
     "srpc_gpu_abi_version": (C.c_int, []),
 }

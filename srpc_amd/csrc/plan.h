@@ -3,6 +3,7 @@
 // var.hip: records with string fields).  Not part of the public ABI.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -76,6 +77,41 @@ struct DeviceGuard {
         if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
     }
 };
+
+// Kernel timing armed by srpc_time_next_call: the data-path kernels of the
+// next C-ABI call on this host thread are launched with hipExtLaunchKernel,
+// which writes the dispatch packet's own begin/end timestamps into the
+// events -- kernel-only time, the same interval rocprofv3 --kernel-trace
+// reports, with no event packets between the launches being timed.
+struct LaunchTimer {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+    bool armed = false;
+    bool started = false;
+};
+
+inline LaunchTimer& launch_timer() {
+    static thread_local LaunchTimer t;
+    return t;
+}
+
+// Disarms the timer when a C-ABI call returns (whatever it launched).
+struct TimedCall {
+    ~TimedCall() { launch_timer() = LaunchTimer{}; }
+};
+
+// Launch a data-path kernel: the first launch of an armed call stamps
+// `start`, every launch stamps `stop` (the last one wins).
+template <typename K, typename... Args>
+inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, Args... args) {
+    LaunchTimer& t = launch_timer();
+    if (t.armed) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t.started ? nullptr : t.start, t.stop, 0u, args...);
+        t.started = true;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
+}
 
 }  // namespace srpc_impl
 

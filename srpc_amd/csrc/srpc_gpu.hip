@@ -488,10 +488,10 @@ int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int 
             const uint64_t grid = cap((nq + per - 1) / per);
             if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
             if (pack)
-                hipLaunchKernelGGL((k_pack_dword_x4<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)),
+                launch(k_pack_dword_x4<W, ITER, NT>, dim3(static_cast<uint32_t>(grid)),
                                    dim3(kBlock), 0, s, m, wire, nq);
             else
-                hipLaunchKernelGGL((k_unpack_dword_x4<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)),
+                launch(k_unpack_dword_x4<W, ITER, NT>, dim3(static_cast<uint32_t>(grid)),
                                    dim3(kBlock), 0, s, m, wire, nq);
             done = nq * 4;
         }
@@ -504,10 +504,10 @@ int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int 
         const uint64_t grid = cap((rest + per - 1) / per);
         if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
         if (pack)
-            hipLaunchKernelGGL((k_pack_dword<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+            launch(k_pack_dword<W, ITER, NT>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
                                0, s, t, wire + done * 4 * W, rest);
         else
-            hipLaunchKernelGGL((k_unpack_dword<W, ITER, NT>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+            launch(k_unpack_dword<W, ITER, NT>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
                                0, s, t, wire + done * 4 * W, rest);
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
@@ -649,6 +649,15 @@ void configure_tile(srpc_plan* p, uint32_t target) {
 extern "C" {
 
 int srpc_gpu_abi_version(void) { return SRPC_GPU_ABI_VERSION; }
+
+int srpc_time_next_call(void* start_event, void* stop_event) {
+    LaunchTimer& t = launch_timer();
+    t = LaunchTimer{};
+    t.start = static_cast<hipEvent_t>(start_event);
+    t.stop = static_cast<hipEvent_t>(stop_event);
+    t.armed = start_event || stop_event;
+    return SRPC_OK;
+}
 
 const char* srpc_status_string(int code) {
     switch (code) {
@@ -799,6 +808,7 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
 
 int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8_t* wire,
                   uint64_t wire_cap, void* stream) {
+    const TimedCall timed;
     if (!p || p->has_string) return SRPC_E_INVALID;  // string schemas: srpc_gpu_pack_var
     if (n == 0) return SRPC_OK;
     if (!wire) return SRPC_E_INVALID;
@@ -817,12 +827,13 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
     const TileArgs a = make_tile_args(p, cols);
     const uint64_t ntiles = (n + p->tile_R - 1) / p->tile_R;
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
-    hipLaunchKernelGGL(k_pack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n, ntiles);
+    launch(k_pack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n, ntiles);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
 int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
                     void* const* cols, srpc_unpack_status* st, void* stream) {
+    const TimedCall timed;
     if (!p || p->has_string) return SRPC_E_INVALID;  // string schemas: srpc_gpu_unpack_var
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
@@ -859,7 +870,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols));
     const uint64_t ntiles = (n_fit + p->tile_R - 1) / p->tile_R;
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
-    hipLaunchKernelGGL(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
+    launch(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     return ret;
 }

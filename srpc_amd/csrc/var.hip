@@ -469,9 +469,9 @@ int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* til
                 hipStream_t s) {
     const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
     if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    hipLaunchKernelGGL(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb);
-    hipLaunchKernelGGL(k_scan_apply<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, nb, out,
+    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial);
+    launch(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb);
+    launch(k_scan_apply<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, nb, out,
                        tile_first, max_tiles);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
@@ -538,6 +538,7 @@ int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_by
 int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_t* const* str_offs, uint64_t n,
                       uint8_t* wire, uint64_t wire_cap, uint64_t* rec_offs, srpc_unpack_status* st,
                       void* scratch, uint64_t scratch_bytes, void* stream) {
+    const TimedCall timed;
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
@@ -560,13 +561,14 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     if (rc) return rc;
     if (n == 0) return SRPC_OK;
     if (!wire) return SRPC_E_INVALID;
-    hipLaunchKernelGGL(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st);
+    launch(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
 int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
                         const uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
                         srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+    const TimedCall timed;
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
@@ -594,7 +596,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     if (n) {
         if (!wire) return SRPC_E_INVALID;
-        hipLaunchKernelGGL(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+        launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
                            wire_len, rec_offs, n, lens, spos, st);
     }
     for (uint32_t f = 0; f < p->nfields; ++f) {
@@ -606,7 +608,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     if (n == 0) return SRPC_OK;
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
-        hipLaunchKernelGGL(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
+        launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
                            tiles + a.sidx[f] * L.max_tiles,
                            spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
     }

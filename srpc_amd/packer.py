@@ -220,6 +220,24 @@ def fill_splitmix_i32(cols: Iterable, n: int, seed: int, first_record: int = 0, 
                                                 _stream(stream)), "srpc_gpu_fill_splitmix_i32")
 
 
+def time_next_call(start=None, stop=None) -> None:
+    """Arm srpc_time_next_call: the kernels of the next pack/unpack call made
+    on this thread stamp their dispatch begin (first kernel) and end (last
+    kernel) into ``start`` / ``stop``.  Each is a torch.cuda.Event created
+    with enable_timing=True and recorded at least once (torch creates the HIP
+    event lazily, on first record), or a raw hipEvent_t handle."""
+    def handle(e):
+        if e is None:
+            return None
+        if hasattr(e, "cuda_event"):
+            if not e.cuda_event:
+                raise ValueError("time_next_call: record the event once first (torch creates it lazily)")
+            return e.cuda_event
+        return int(e)
+
+    check(_lib.lib().srpc_time_next_call(handle(start), handle(stop)), "srpc_time_next_call")
+
+
 __all__ = ["Schema", "GpuPacker", "SrpcError", "request_prefix", "response_prefix",
-           "fill_splitmix_i32", "BOOL", "INT8", "CHAR", "INT16", "INT32", "INT64", "STRING",
+           "fill_splitmix_i32", "time_next_call", "BOOL", "INT8", "CHAR", "INT16", "INT32", "INT64", "STRING",
            "RPC_SUCCESS", "RPC_ERR_FUNCTION_NOT_REGISTERED", "RPC_ERR_RECV_TIMEOUT"]

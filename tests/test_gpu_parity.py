@@ -277,6 +277,39 @@ def test_fill_splitmix_matches_numpy():
 
 # ---- full BASELINE.json sizes ----------------------------------------------------
 
+@pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
+def test_kernel_timing_hook(path):
+    """srpc_time_next_call: the armed call's kernels stamp begin/end into the
+    events, the bytes are unchanged, and the hook is consumed by one call."""
+    n = 1 << 20
+    cols = oracle.splitmix_columns_i32(4, n, 0x5EED)
+    p = GpuPacker(QUAD)
+    p.force_path(path)
+    dcols = [dev(c) for c in cols]
+    wire = empty(n * 16)
+    back = [empty(n * 4) for _ in range(4)]
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    for e in ev:
+        e.record(s)
+    torch.cuda.synchronize()
+    srpc_amd.time_next_call(ev[0], ev[1])
+    p.pack(dcols, n, wire, stream=s)
+    srpc_amd.time_next_call(ev[2], ev[3])
+    p.unpack(wire, n * 16, n, back, stream=s)
+    ev[4].record(s)
+    p.pack(dcols, n, wire, stream=s)  # not armed: must not restamp ev[3]
+    torch.cuda.synchronize()
+    t_pack, t_unpack = ev[0].elapsed_time(ev[1]), ev[2].elapsed_time(ev[3])
+    assert 0 < t_pack < 100 and 0 < t_unpack < 100
+    assert ev[3].elapsed_time(ev[4]) >= 0
+    assert host(wire, n * 16).tobytes() == oracle.pack([oracle.INT32] * 4, cols, n)
+    for c, b in zip(cols, back):
+        np.testing.assert_array_equal(host(b, n * 4, np.int32), c)
+    with pytest.raises(ValueError):
+        srpc_amd.time_next_call(torch.cuda.Event(enable_timing=True), None)
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("label", ["quad_body_16M", "quad_body_64M"])
 def test_quad_full_size_digest_and_roundtrip(manifest, label):

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Throughput of every kernel family on representative schemas (one MI355X).
 
-For each case: pack and unpack of N records through the C ABI, timed with
-HIP events on the launch stream (median of R reps after warm-up), reported
+For each case: pack and unpack of N records through the C ABI, timed on the
+kernel clock of srpc_time_next_call (dispatch begin of the call's first
+kernel to end of its last; median of R reps after warm-up), reported
 as algorithmic GB/s (columns + wire bytes moved once) and fraction of the
 8 TB/s HBM3E peak.  Every case is first checked bit-exact against the CPU
 oracle on a 4096-record prefix of the same inputs.
@@ -43,12 +44,14 @@ def main():
         for _ in range(3):
             fn()
         ts = []
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        b.record(s)
         for _ in range(args.reps):
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record(s)
+            # kernel clock: the call's first kernel begin -> last kernel end
+            srpc_amd.time_next_call(a, b)
             fn()
-            b.record(s)
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b) / 1e3)
         return statistics.median(ts)

@@ -3,8 +3,8 @@
 
 Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
 every variant is timed once per round, rounds repeat, and the median and min
-per variant are reported.  Each kernel is bracketed by its own HIP events on
-the launch stream.  "cold" rounds write a 1 GiB scratch buffer before each
+per variant are reported.  Each pack/unpack is timed on the kernel clock of
+srpc_time_next_call (dispatch begin/end); the torch copy by events around it.  "cold" rounds write a 1 GiB scratch buffer before each
 timed kernel so the 256 MiB Infinity Cache holds none of its inputs.
 
 Known-good reference on the same device: torch's device-to-device copy of the
@@ -64,14 +64,18 @@ def main():
         variants.append(("tile", 0, 0, 0, 0))
     alg = 2 * 4 * F * n  # bytes per kernel: read F*4 + write F*4 per record
 
-    def timed(fn, cold):
+    def timed(fn, cold, hook=True):
         if cold:
             flush.fill_(1)
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(s)
+        if hook:  # kernel clock (srpc_time_next_call) restamps a and b
+            b.record(s)
+            srpc_amd.time_next_call(a, b)
         fn()
-        b.record(s)
+        if not hook:
+            b.record(s)
         return a, b
 
     res = {}
@@ -89,7 +93,7 @@ def main():
                 set_variant(p, v, srpc_amd)
                 evs.append((v, "pack", timed(lambda: p.pack(cols, n, wire, stream=s), cold)))
                 evs.append((v, "unpack", timed(lambda: p.unpack(wire, wire.numel(), n, back, stream=s), cold)))
-            evs.append((("copy",), "d2d", timed(lambda: copy_dst.copy_(copy_src), cold)))
+            evs.append((("copy",), "d2d", timed(lambda: copy_dst.copy_(copy_src), cold, hook=False)))
             torch.cuda.synchronize()
             for v, k, (a, b) in evs:
                 res.setdefault((v, k, cold), []).append(a.elapsed_time(b))
