@@ -440,12 +440,14 @@ def _random_string_batch(kinds, n, rng, maxlen):
 @pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 2047, 2048, 2049, 30_001])
 @pytest.mark.parametrize("schema,maxlen,envelope", [
     ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
-    ("nested", 64, "response")])
+    ("nested", 64, "response"), ("wide", 24, "request")])
 def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
     kinds = {"s": [oracle.STRING],
              "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
              "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
-             "nested": [oracle.INT64, oracle.INT8, oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]}[schema]
+             "nested": [oracle.INT64, oracle.INT8, oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING],
+             "wide": [oracle.STRING, oracle.INT8, oracle.INT16, oracle.STRING, oracle.INT32, oracle.INT64,
+                      oracle.BOOL, oracle.STRING, oracle.CHAR, oracle.INT64, oracle.INT8]}[schema]
     if maxlen > 1000 and n > 3000:
         n = 3000
     rng = np.random.default_rng(n + maxlen)
@@ -470,6 +472,39 @@ def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
         assert back[f].tobytes() == ocols[f].tobytes(), f
         if k == oracle.STRING:
             assert np.array_equal(boffs[f], ooffs[f])
+
+
+@pytest.mark.parametrize("chars_shift,offs_shift", [(0, 0), (3, 8), (15, 8), (1, 0)])
+def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift):
+    """Chars columns and offset arrays at any byte / 8-byte alignment, strings
+    far longer than a 4 KiB tile, and a tiny-record run (many records per tile)."""
+    kinds = [oracle.INT8, oracle.STRING, oracle.INT16]
+    rng = np.random.default_rng(chars_shift * 31 + offs_shift)
+    n = 3000
+    lens = rng.integers(0, 24, n).astype(np.uint64)
+    lens[100] = 70_000
+    lens[101] = 9_000
+    lens[2000:2600] = 0
+    o = np.zeros(n + 1, np.uint64)
+    o[1:] = np.cumsum(lens)
+    chars = rng.integers(0, 256, int(o[-1]), dtype=np.uint8)
+    c8 = rng.integers(-128, 128, n, dtype=np.int8)
+    c16 = rng.integers(-2**15, 2**15, n, dtype=np.int16)
+    p = GpuPacker(Schema("U", (("a", oracle.INT8), ("s", oracle.STRING), ("b", oracle.INT16))))
+    want = oracle.pack(kinds, [c8, chars, c16], n, b"", [None, o, None])
+    dchars = torch.zeros(len(chars) + 32, dtype=torch.uint8, device=DEV)
+    dchars[chars_shift:chars_shift + len(chars)].copy_(torch.from_numpy(chars))
+    doffs = torch.zeros(8 * (n + 1) + 16, dtype=torch.uint8, device=DEV)
+    doffs[offs_shift:offs_shift + 8 * (n + 1)].copy_(torch.from_numpy(o.view(np.uint8)))
+    wire = empty(len(want) + 16)
+    rec = empty(8 * (n + 1))
+    sb = p.var_scratch_bytes(n, len(want))
+    scratch = empty(sb + 16)
+    st = status_buf()
+    p.pack_var([dev(c8), dchars[chars_shift:], dev(c16)], [None, doffs[offs_shift:], None], n, wire,
+               len(want), rec, scratch, sb, st)
+    assert read_status(st) == (0, 2**64 - 1)
+    assert host(wire, len(want)).tobytes() == want
 
 
 def test_strings_errors():
