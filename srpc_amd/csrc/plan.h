@@ -124,7 +124,8 @@ struct srpc_plan {
     uint32_t off[srpc_impl::kMaxFields] = {};   // offset within record, prefix included
     uint32_t prefix_len = 0;
     uint8_t h_prefix[srpc_impl::kMaxPrefix] = {};
-    uint8_t* d_prefix = nullptr;
+    uint8_t* d_prefix = nullptr;       // device copy (d_prefix_alloc + 16, zero-padded 16 B each side)
+    uint8_t* d_prefix_alloc = nullptr;
     uint64_t stride = 0;             // fixed record bytes (0 for string schemas)
     bool has_string = false;
     bool dword_ok = false;

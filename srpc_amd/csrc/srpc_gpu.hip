@@ -644,6 +644,25 @@ void configure_tile(srpc_plan* p, uint32_t target) {
     p->tile_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
 }
 
+// Device copy of the constant prefix with 16 zero bytes on both sides, so a
+// 16-byte load at any offset in [-15, prefix_len) stays inside the buffer.
+int upload_prefix(srpc_plan* p) {
+    if (!p->prefix_len) return SRPC_OK;
+    const size_t bytes = p->prefix_len + 32;
+    if (hipMalloc(&p->d_prefix_alloc, bytes) != hipSuccess) {
+        p->d_prefix_alloc = nullptr;
+        return SRPC_E_HIP;
+    }
+    if (hipMemset(p->d_prefix_alloc, 0, bytes) != hipSuccess ||
+        hipMemcpy(p->d_prefix_alloc + 16, p->h_prefix, p->prefix_len, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(p->d_prefix_alloc);
+        p->d_prefix_alloc = nullptr;
+        return SRPC_E_HIP;
+    }
+    p->d_prefix = p->d_prefix_alloc + 16;
+    return SRPC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -708,13 +727,9 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         p->fixed_bytes = static_cast<uint32_t>(o + 8ull * p->nstrings);
         p->stride = 0;
         DeviceGuard g(device);
-        if (p->prefix_len) {
-            if (hipMalloc(&p->d_prefix, p->prefix_len) != hipSuccess ||
-                hipMemcpy(p->d_prefix, p->h_prefix, p->prefix_len, hipMemcpyHostToDevice) != hipSuccess) {
-                if (p->d_prefix) (void)hipFree(p->d_prefix);
-                delete p;
-                return SRPC_E_HIP;
-            }
+        if (upload_prefix(p) != SRPC_OK) {
+            delete p;
+            return SRPC_E_HIP;
         }
         *out = p;
         return SRPC_OK;
@@ -728,13 +743,9 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         return SRPC_E_UNSUPPORTED;
     }
     DeviceGuard g(device);
-    if (p->prefix_len) {
-        if (hipMalloc(&p->d_prefix, p->prefix_len) != hipSuccess ||
-            hipMemcpy(p->d_prefix, p->h_prefix, p->prefix_len, hipMemcpyHostToDevice) != hipSuccess) {
-            if (p->d_prefix) (void)hipFree(p->d_prefix);
-            delete p;
-            return SRPC_E_HIP;
-        }
+    if (upload_prefix(p) != SRPC_OK) {
+        delete p;
+        return SRPC_E_HIP;
     }
     if (p->dword_ok) p->dv = default_dword_variant(static_cast<uint32_t>(o / 4));
     // TILE image size: 32 KiB, the best or within 3 % of the best of 4-48 KiB
@@ -746,9 +757,9 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
 
 int srpc_plan_destroy(srpc_plan* p) {
     if (!p) return SRPC_E_INVALID;
-    if (p->d_prefix) {
+    if (p->d_prefix_alloc) {
         DeviceGuard g(p->device);
-        (void)hipFree(p->d_prefix);
+        (void)hipFree(p->d_prefix_alloc);
     }
     delete p;
     return SRPC_OK;

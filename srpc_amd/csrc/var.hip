@@ -11,12 +11,13 @@
 //      rec_offs[0..n] (u64).  Inside a workgroup: per-thread serial scan of 8
 //      items, a 64-lane wavefront scan of the thread totals (__shfl_up), and
 //      an LDS scan of the 4 wave totals.
-//   2. k_pack_var: the wire is cut into 4 KiB tiles; a tile's first record is
-//      found by a binary search of rec_offs, the next record starts are staged
-//      in LDS, and every lane builds one 16-byte chunk of output: it walks the
-//      records/segments (prefix, fixed fields, string length, string bytes)
-//      covering its 16 bytes, assembles them in an LDS staging slot and
-//      writes them with one 16-byte store.
+//   2. k_pack_var: the wire is cut into 4 KiB tiles; a tile's first record
+//      comes from the table the scan wrote (tile_first), the starts of the
+//      records up to the next tile's first one are staged in LDS, and every
+//      lane builds one 16-byte chunk of output: it walks the records/segments
+//      (prefix, fixed fields, string length, string bytes) covering its 16
+//      bytes, assembles them in an LDS staging slot and writes them with one
+//      16-byte store.
 // UNPACK (srpc_gpu_unpack_var) -- needs the record start index rec_offs
 //   (produced by pack, or by frame lengths on a socket):
 //   1. k_unpack_var_walk: one record per lane: prefix check, fixed fields to
@@ -37,6 +38,8 @@
 
 namespace srpc_impl {
 namespace {
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 2048 items
@@ -191,8 +194,11 @@ struct Window {
     uint32_t len;  // entries valid in win[0..len)
 };
 
-__device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, uint64_t r0, uint64_t* win) {
-    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(kWindow, n + 1 - r0));
+// rz: the record covering the next tile's first byte (or n - 1): entries
+// r0 .. rz + 1 cover every byte of this tile, so only those are staged.
+__device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, uint64_t r0, uint64_t rz,
+                                              uint64_t* win) {
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(min<uint64_t>(kWindow, n + 1 - r0), rz + 2 - r0));
     for (uint32_t k = threadIdx.x; k < len; k += kBlock) win[k] = offs[r0 + k];
     __syncthreads();
     return {r0, len};
@@ -200,8 +206,8 @@ __device__ __forceinline__ Window load_window(const uint64_t* offs, uint64_t n, 
 
 // The window plus the same records' entries of a second offsets array.
 __device__ __forceinline__ Window load_window2(const uint64_t* offs, const uint64_t* offs2, uint64_t n, uint64_t r0,
-                                               uint64_t* win, uint64_t* win2) {
-    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(kWindow, n + 1 - r0));
+                                               uint64_t rz, uint64_t* win, uint64_t* win2) {
+    const uint32_t len = static_cast<uint32_t>(min<uint64_t>(min<uint64_t>(kWindow, n + 1 - r0), rz + 2 - r0));
     for (uint32_t k = threadIdx.x; k < len; k += kBlock) {
         win[k] = offs[r0 + k];
         win2[k] = offs2[r0 + k];
@@ -227,18 +233,39 @@ __device__ __forceinline__ uint64_t find_record(const uint64_t* offs, uint64_t n
 }
 
 // ---- byte movers ----------------------------------------------------------------
-// gfx950 runs in unaligned-access mode: a 16-byte memcpy from any address is
-// one global_load_dwordx4, to any LDS address one (or a few) ds_write.  Every
-// copy below moves <= 16 bytes with ONE such load, so a chunk costs one load
-// per record segment it touches instead of one per byte.  Sources are never
-// read past their end (`end`): near it the copy falls back to bytes.
-__device__ __forceinline__ void copy_le16(uint8_t* dst, const uint8_t* src, uint32_t k, const uint8_t* end) {
+// Every output chunk (16 aligned bytes) is assembled in a 32-byte LDS slot of
+// its lane -- one unaligned 16-byte global load and one 16-byte LDS write per
+// record segment it touches -- and leaves with one 16-byte store.  (Merging
+// in registers instead -- the load taken from src - b so the segment lands in
+// place, then a byte mask -- measured 1.4-1.6x slower: profiles/r01_paths.log.)
+// Sources are never read past their end (`end`): near it the copy falls back
+// to bytes.
+struct Slot {
+    uint8_t* s;
+};
+
+__device__ __forceinline__ void put(Slot& c, const uint8_t* src, int b, int k, const uint8_t* end) {
     if (src + 16 <= end) {
         uint4 v;
         __builtin_memcpy(&v, src, 16);
-        __builtin_memcpy(dst, &v, 16);  // dst has 16 bytes of room (32-byte slots)
+        __builtin_memcpy(c.s + b, &v, 16);  // the slot has 16 bytes of room past any b < 16
     } else {
-        for (uint32_t i = 0; i < k; ++i) dst[i] = src[i];
+        for (int i = 0; i < k; ++i) c.s[b + i] = src[i];
+    }
+}
+
+// Bytes [x, x + 8) of a u64 string length at slot byte b.
+__device__ __forceinline__ void put_u64(Slot& c, uint64_t v, int x, int b) {
+    v >>= 8 * x;
+    __builtin_memcpy(c.s + b, &v, 8);
+}
+
+__device__ __forceinline__ void store_slot(uint8_t* dst, const Slot& c, uint32_t nb) {
+    if (nb == 16) {
+        const u64x2 v = *reinterpret_cast<const u64x2*>(c.s);
+        __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(dst));
+    } else {
+        for (uint32_t i = 0; i < nb; ++i) dst[i] = c.s[i];
     }
 }
 
@@ -250,20 +277,17 @@ __device__ __forceinline__ T load_unaligned(const uint8_t* p) {
 }
 
 // ---- pack ---------------------------------------------------------------------
-// Write `cnt` (<= 16) bytes of record r, from byte q of the record, to dst
-// (an LDS slot with 16 bytes of slack after dst).  Segments in wire order:
-// prefix, then every field (fixed value | u64 length, chars).
-// sw (may be null): LDS copy of soff[f0][r], soff[f0][r+1] for the first string field f0.
-__device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_t* pre, const uint64_t* climit,
-                                                  uint32_t f0, const uint64_t* sw, uint64_t n, uint64_t r, uint64_t q,
-                                                  uint32_t cnt, uint8_t* dst) {
+// Merge `cnt` (<= 16) bytes of record r, from byte q of the record, into chunk
+// bytes [b, b + cnt).  Segments in wire order: prefix, then every field
+// (fixed value | u64 length, chars).  sw (may be null): LDS copy of
+// soff[f0][r], soff[f0][r+1] for the first string field f0.
+__device__ __forceinline__ void emit_record(const VarArgs& a, const uint64_t* climit, uint32_t f0, const uint64_t* sw,
+                                            uint64_t n, uint64_t r, uint64_t q, uint32_t cnt, int b, Slot& c) {
     const uint64_t end = q + cnt;
     if (q < a.prefix_len) {
-        const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, a.prefix_len) - q);
-        uint4 v;
-        __builtin_memcpy(&v, pre + q, 16);  // pre has 16 bytes of slack
-        __builtin_memcpy(dst, &v, 16);
-        dst += k;
+        const int k = static_cast<int>(min<uint64_t>(end, a.prefix_len) - q);
+        put(c, a.prefix + q, b, k, a.prefix + a.prefix_len + 16);
+        b += k;
         q += k;
     }
     uint64_t s = a.prefix_len;  // start of the current segment within the record
@@ -271,9 +295,9 @@ __device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_
         const uint32_t sz = a.size[f];
         if (sz) {
             if (q < s + sz) {
-                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + sz) - q);
-                copy_le16(dst, a.col[f] + r * sz + (q - s), k, a.col[f] + n * sz);
-                dst += k;
+                const int k = static_cast<int>(min<uint64_t>(end, s + sz) - q);
+                put(c, a.col[f] + r * sz + (q - s), b, k, a.col[f] + n * sz);
+                b += k;
                 q += k;
             }
             s += sz;
@@ -282,17 +306,16 @@ __device__ __forceinline__ void emit_record_bytes(const VarArgs& a, const uint8_
             const uint64_t b0 = staged ? sw[0] : a.soff[f][r];
             const uint64_t len = (staged ? sw[1] : a.soff[f][r + 1]) - b0;
             if (q < s + 8) {
-                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + 8) - q);
-                const uint64_t v = len >> (8 * (q - s));
-                __builtin_memcpy(dst, &v, 8);
-                dst += k;
+                const int k = static_cast<int>(min<uint64_t>(end, s + 8) - q);
+                put_u64(c, len, static_cast<int>(q - s), b);
+                b += k;
                 q += k;
             }
             s += 8;
             if (q < end && q < s + len) {
-                const uint32_t k = static_cast<uint32_t>(min<uint64_t>(end, s + len) - q);
-                copy_le16(dst, a.col[f] + b0 + (q - s), k, a.col[f] + climit[f]);
-                dst += k;
+                const int k = static_cast<int>(min<uint64_t>(end, s + len) - q);
+                put(c, a.col[f] + b0 + (q - s), b, k, a.col[f] + climit[f]);
+                b += k;
                 q += k;
             }
             s += len;
@@ -307,11 +330,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     __shared__ uint64_t win[kWindow];
     __shared__ uint64_t swin[kWindow];       // char offsets of the first string field, same records
     __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     uint32_t f0 = 0;                         // the first string field
     while (a.size[f0]) ++f0;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
-    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
-    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
     for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
     const uint64_t total = rec_offs[n];
     const uint64_t limit = min(total, wire_cap);
@@ -320,30 +341,27 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
-        const Window w = load_window2(rec_offs, a.soff[f0], n, tile_first[t], win, swin);
+        const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
+        const Window w = load_window2(rec_offs, a.soff[f0], n, r0, rz, win, swin);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
-            uint8_t* slot = stage + 32 * threadIdx.x;
             uint64_t r = find_record(rec_offs, n, w, win, p0);
             uint64_t p = p0;
             uint32_t b = 0;
+            Slot c{slots + 32 * threadIdx.x};
             while (b < nb && r < n) {
                 const uint64_t k = r - w.r0;
                 const uint64_t rs = k + 1 < w.len ? win[k] : rec_offs[r];
                 const uint64_t re = k + 1 < w.len ? win[k + 1] : rec_offs[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                emit_record_bytes(a, pre, climit, f0, k + 1 < w.len ? swin + k : nullptr, n, r, p - rs, cnt,
-                                  slot + b);
+                emit_record(a, climit, f0, k + 1 < w.len ? swin + k : nullptr, n, r, p - rs, cnt,
+                            static_cast<int>(b), c);
                 b += cnt;
                 p += cnt;
                 ++r;
             }
-            if (nb == 16) {
-                *reinterpret_cast<uint4*>(wire + p0) = *reinterpret_cast<const uint4*>(slot);
-            } else {
-                for (uint32_t i = 0; i < nb; ++i) wire[p0 + i] = slot[i];
-            }
+            store_slot(wire + p0, c, nb);
         }
         __syncthreads();  // the window is rewritten for the next tile
     }
@@ -420,34 +438,32 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
                                                              const uint64_t* __restrict__ spos, uint64_t n,
                                                              uint8_t* __restrict__ chars) {
     __shared__ uint64_t win[kWindow];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kBlock * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
-        const Window w = load_window(soff, n, tile_first[t], win);
+        const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
+        const Window w = load_window(soff, n, r0, rz, win);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < total) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
-            uint8_t* slot = stage + 32 * threadIdx.x;
             uint64_t r = find_record(soff, n, w, win, p0);
             uint64_t p = p0;
             uint32_t b = 0;
+            Slot c{slots + 32 * threadIdx.x};
             while (b < nb && r < n) {
                 const uint64_t k = r - w.r0;
                 const uint64_t rs = k + 1 < w.len ? win[k] : soff[r];
                 const uint64_t re = k + 1 < w.len ? win[k + 1] : soff[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                if (cnt) copy_le16(slot + b, wire + spos[r] + (p - rs), cnt, wire + wire_len);
+                if (cnt)
+                    put(c, wire + spos[r] + (p - rs), static_cast<int>(b), static_cast<int>(cnt), wire + wire_len);
                 b += cnt;
                 p += cnt;
                 ++r;
             }
-            if (nb == 16) {
-                *reinterpret_cast<uint4*>(chars + p0) = *reinterpret_cast<const uint4*>(slot);
-            } else {
-                for (uint32_t i = 0; i < nb; ++i) chars[p0 + i] = slot[i];
-            }
+            store_slot(chars + p0, c, nb);
         }
         __syncthreads();
     }
@@ -609,8 +625,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
-                           tiles + a.sidx[f] * L.max_tiles,
-                           spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
+               tiles + a.sidx[f] * L.max_tiles, spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
