@@ -35,15 +35,34 @@ def build_all() -> list[str]:
     return built
 
 
+BATCHGEN_CONTRACT = os.path.join(HERE, "batchgen_example.contract")
+BATCHGEN_HEADER = os.path.join(OUT, "batchgen_example_batch.hpp")
+
+
+def generate_batch_header() -> str:
+    """srpc_amd.batchgen over the example contract (message structs included)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from srpc_amd import batchgen
+    os.makedirs(OUT, exist_ok=True)
+    text = batchgen.generate(batchgen.parse(open(BATCHGEN_CONTRACT).read()), "batchgen_example.contract",
+                             messages=True)
+    if not os.path.exists(BATCHGEN_HEADER) or open(BATCHGEN_HEADER).read() != text:
+        with open(BATCHGEN_HEADER, "w") as f:
+            f.write(text)
+    return BATCHGEN_HEADER
+
+
 def build_one(src: str) -> str:
     os.makedirs(OUT, exist_ok=True)
     exe = exe_path(src)
     req = needs(src)
-    if os.path.exists(exe) and os.path.getmtime(exe) > max(
-            os.path.getmtime(p) for p in [src] + glob.glob(os.path.join(ROOT, "include", "**", "*"),
-                                                           recursive=True) if os.path.isfile(p)):
+    deps = [src] + glob.glob(os.path.join(ROOT, "include", "**", "*"), recursive=True)
+    if "batchgen" in req:
+        deps.append(generate_batch_header())
+    if os.path.exists(exe) and os.path.getmtime(exe) > max(os.path.getmtime(p) for p in deps if os.path.isfile(p)):
         return exe
-    cmd = ["g++", "-std=c++20", "-O2", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
+    cmd = ["g++", "-std=c++20", "-O2", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"), "-I", OUT,
            "-o", exe, src]
     if "reference" in req:
         cmd += ["-I", os.path.join(REF, "examples"), "-Wno-unused-parameter"]
