@@ -84,10 +84,13 @@ def lib() -> C.CDLL:
     global _lib
     with _lock:
         if _lib is None:
-            if _build.needs_build():
-                _build.build()
+            path = os.environ.get("SRPC_GPU_LIB")  # A/B experiments: another build of the library
+            if not path:
+                if _build.needs_build():
+                    _build.build()
+                path = _build.SO
             _preload_torch()
-            so = C.CDLL(_build.SO, mode=C.RTLD_GLOBAL)
+            so = C.CDLL(path, mode=C.RTLD_GLOBAL)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(so, name)
                 fn.restype = res
@@ -97,7 +100,7 @@ def lib() -> C.CDLL:
 
 
 def so_path() -> str:
-    return os.path.abspath(_build.SO)
+    return os.path.abspath(os.environ.get("SRPC_GPU_LIB") or _build.SO)
 
 
 def status_string(code: int) -> str:

@@ -39,21 +39,25 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, srcdir: str | None = None,
+          defines: tuple[str, ...] = ()) -> str:
+    """Compile csrc/*.hip into SO (or `out`, from `srcdir`, with -D`defines`: A/B builds)."""
+    if out is None and not force and not needs_build():
         return SO
-    tmp = SO + ".tmp"
+    target = out or SO
+    src = sorted(glob.glob(os.path.join(srcdir, "*.hip"))) if srcdir else sources()
+    inc = srcdir or os.path.join(PKG, "csrc")
+    tmp = target + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-command-line-argument",
-           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc"),
-           "-o", tmp] + sources()
+           "-I", os.path.join(ROOT, "include"), "-I", inc] + [f"-D{d}" for d in defines] + ["-o", tmp] + src
     if verbose:
         print(" ".join(cmd))
     out = subprocess.run(cmd, capture_output=True, text=True)
     if out.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + out.stdout + out.stderr)
-    os.replace(tmp, SO)
-    return SO
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

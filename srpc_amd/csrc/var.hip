@@ -276,6 +276,27 @@ __device__ __forceinline__ T load_unaligned(const uint8_t* p) {
     return v;
 }
 
+// ---- phase clock (A/B diagnostics, compiled only with -DSRPC_PHASES) -------------
+#ifdef SRPC_PHASES
+__device__ unsigned long long g_phase[8];
+#define PHASE_BEGIN uint64_t ph_last_ = clock64(), ph_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PHASE(i)                                       \
+    do {                                               \
+        const uint64_t now_ = clock64();               \
+        ph_acc_[i] += now_ - ph_last_;                 \
+        ph_last_ = now_;                               \
+    } while (0)
+#define PHASE_COUNT(i) ph_acc_[i] += 1
+#define PHASE_END                                                              \
+    if (threadIdx.x == 0)                                                      \
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phase[i_], ph_acc_[i_]);
+#else
+#define PHASE_BEGIN
+#define PHASE(i)
+#define PHASE_COUNT(i)
+#define PHASE_END
+#endif
+
 // ---- pack ---------------------------------------------------------------------
 // Merge `cnt` (<= 16) bytes of record r, from byte q of the record, into chunk
 // bytes [b, b + cnt).  Segments in wire order: prefix, then every field
@@ -339,14 +360,18 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
         report_bad(st, SRPC_STATUS_BOUNDS, upper_index(rec_offs, n, wire_cap));
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
+    PHASE_BEGIN
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
         const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
+        PHASE(0);
         const Window w = load_window2(rec_offs, a.soff[f0], n, r0, rz, win, swin);
+        PHASE(1);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, limit - p0));
             uint64_t r = find_record(rec_offs, n, w, win, p0);
+            PHASE(2);
             uint64_t p = p0;
             uint32_t b = 0;
             Slot c{slots + 32 * threadIdx.x};
@@ -361,10 +386,15 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
                 p += cnt;
                 ++r;
             }
+            PHASE(3);
             store_slot(wire + p0, c, nb);
+            PHASE(4);
         }
         __syncthreads();  // the window is rewritten for the next tile
+        PHASE(5);
+        PHASE_COUNT(6);
     }
+    PHASE_END
 }
 
 // ---- unpack -------------------------------------------------------------------
@@ -540,6 +570,19 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
 using namespace srpc_impl;
 
 extern "C" {
+
+#ifdef SRPC_PHASES
+int srpc_debug_phases(uint64_t* host8, int reset) {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return SRPC_E_HIP;
+    for (int i = 0; i < 8; ++i) host8[i] = h[i];
+    if (reset) {
+        const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return SRPC_E_HIP;
+    }
+    return SRPC_OK;
+}
+#endif
 
 int srpc_plan_var_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_bytes, uint64_t* out) {
     if (!p || !out) return SRPC_E_INVALID;
