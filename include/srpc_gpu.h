@@ -124,6 +124,9 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_NONTEMPORAL 3      /* bit0 non-temporal stores, bit1 loads      */
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
                                         (1024..49152)                            */
+#define SRPC_TUNE_TILE_KERNEL 6      /* TILE path kernel: 0 = LDS image (stride-S
+                                        scatter/gather), 1 = register-assembled
+                                        16-byte chunks from aligned column slabs */
 #define SRPC_TUNE_GRID 5             /* DWORD path: max workgroups (0 = one per
                                         256*iter records; else grid-stride)       */
 int srpc_plan_tune(srpc_plan* plan, int knob, int value);

@@ -1,6 +1,7 @@
 // plan.h -- internal: the srpc_plan object and helpers shared by the kernel
 // translation units of libsrpc_gpu.so (srpc_gpu.hip: fixed-size records,
-// var.hip: records with string fields).  Not part of the public ABI.
+// chunk.hip: the TILE path's register-assembled kernels, var.hip: records
+// with string fields).  Not part of the public ABI.
 #pragma once
 
 #include <hip/hip_ext.h>
@@ -113,6 +114,28 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
     }
 }
 
+// TILE path, CHUNK kernel (chunk.hip): kernel arguments and the plan's table.
+struct ChunkArgs {
+    const uint8_t* col[kMaxFields];  // field columns (pack: sources, unpack: destinations)
+    uint32_t lg[kMaxFields];         // log2(field size)
+    uint32_t slab_off[kMaxFields];   // LDS slab of each field: R * (bytes of the fields before)
+    const uint8_t* table;            // device blob: tmpl[P][16] | pmask[P][16] | ent[P][emax]
+    uint32_t table_bytes;            // multiple of 16
+    uint32_t slab_bytes;             // R * field bytes (multiple of 16)
+    uint32_t nfields, stride, prefix_len, R, P, rpp, emax;
+};
+
+// An occurrence of a field in a chunk phase: record q of the period, log2
+// size, first byte at chunk position pos (-7..15), the field's LDS slab.
+inline uint32_t chunk_entry(uint32_t q, uint32_t lg, int pos, uint32_t slab) {
+    return q | lg << 8 | static_cast<uint32_t>(pos + 8) << 10 | slab << 15;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_chunk(ChunkArgs a, uint8_t* __restrict__ wire, uint64_t n,
+                                                       uint64_t ntiles);
+__global__ __launch_bounds__(kBlock) void k_unpack_chunk(ChunkArgs a, const uint8_t* __restrict__ wire, uint64_t n,
+                                                         uint64_t ntiles, srpc_unpack_status* st);
+
 }  // namespace srpc_impl
 
 // The object behind the opaque srpc_plan* of include/srpc_gpu.h.
@@ -133,6 +156,12 @@ struct srpc_plan {
     uint32_t tile_R = 0, tile_L = 0;
     int tile_grid = 0;               // resident workgroups for grid-stride tiles
     size_t tile_lds = 0;
+    int tile_kernel = 0;             // SRPC_TUNE_TILE_KERNEL: 0 LDS image, 1 register-assembled chunks
+    uint8_t* d_chunk = nullptr;      // CHUNK table blob (ChunkArgs::table), nullptr = not eligible
+    uint32_t chunk_table_bytes = 0, chunk_slab_bytes = 0, chunk_P = 0, chunk_rpp = 0, chunk_emax = 0;
+    uint32_t chunk_slab_off[srpc_impl::kMaxFields] = {};
+    int chunk_grid = 0;
+    size_t chunk_lds = 0;
     bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
     srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
     // string schemas (SRPC_PATH_VAR)

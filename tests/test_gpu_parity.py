@@ -26,6 +26,23 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
 DEV = torch.device("cuda:0")
 
 
+@pytest.fixture(params=[0, 1], ids=["image", "chunk"])
+def tile_kernel(request, monkeypatch):
+    """Run a test once per TILE-path kernel: every GpuPacker made in it gets
+    that kernel (plans whose table does not fit keep the image kernel)."""
+    init = GpuPacker.__init__
+
+    def patched(self, *a, **kw):
+        init(self, *a, **kw)
+        if self.record_bytes:
+            try:
+                self.tune(tile_kernel=request.param)
+            except srpc_amd.SrpcError:
+                assert request.param == 1
+    monkeypatch.setattr(GpuPacker, "__init__", patched)
+    return request.param
+
+
 def dev(a: np.ndarray) -> "torch.Tensor":
     """numpy -> device tensor with the same bytes (16-byte aligned allocation)."""
     b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
@@ -79,7 +96,7 @@ SIZES = [0, 1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 4096 + 17, 100_00
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
 @pytest.mark.parametrize("n", SIZES)
-def test_quad_pack_unpack_vs_oracle(n, path):
+def test_quad_pack_unpack_vs_oracle(n, path, tile_kernel):
     p = GpuPacker(QUAD)
     assert p.path == SRPC_PATH_DWORD
     p.force_path(path)
@@ -93,7 +110,7 @@ def test_quad_pack_unpack_vs_oracle(n, path):
 
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
-def test_quad_golden_head_and_edges(golden_dir, path):
+def test_quad_golden_head_and_edges(golden_dir, path, tile_kernel):
     p = GpuPacker(QUAD)
     p.force_path(path)
     cols = oracle.splitmix_columns_i32(4, 4096)
@@ -107,7 +124,7 @@ def test_quad_golden_head_and_edges(golden_dir, path):
 
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
-def test_number_and_two_numbers(golden_dir, manifest, path):
+def test_number_and_two_numbers(golden_dir, manifest, path, tile_kernel):
     p = GpuPacker(NUMBER)
     p.force_path(path)
     n = manifest["streams"]["number_body_1M"]["records"]
@@ -128,7 +145,7 @@ ALL_KINDS = Schema.of("all_kinds", ("k_bool", "bool"), ("k_i8", "int8"), ("k_cha
 ALL_DT = [np.uint8, np.int8, np.int8, np.int16, np.int32, np.int64]
 
 
-def test_all_kinds_tile(golden_dir):
+def test_all_kinds_tile(golden_dir, tile_kernel):
     p = GpuPacker(ALL_KINDS)
     assert p.path == SRPC_PATH_TILE and p.record_bytes == 17
     z = np.load(os.path.join(golden_dir, "all_kinds_in.npz"))
@@ -143,7 +160,7 @@ def test_all_kinds_tile(golden_dir):
 
 @pytest.mark.parametrize("n", [1, 7, 16, 17, 333, 4099, 65537])
 @pytest.mark.parametrize("schema", ["all", "i16x3", "i64x2", "i8", "mixed_dword"])
-def test_random_schemas_vs_oracle(n, schema):
+def test_random_schemas_vs_oracle(n, schema, tile_kernel):
     kinds = {"all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
              "i16x3": [oracle.INT16] * 3, "i64x2": [oracle.INT64] * 2, "i8": [oracle.INT8],
              "mixed_dword": [oracle.INT64, oracle.INT32, oracle.INT64]}[schema]
@@ -189,7 +206,7 @@ def test_dword_variants_identical(schema):
 
 # ---- envelopes (Calculator.square) ---------------------------------------------
 
-def test_square_request_envelope(golden_dir, manifest):
+def test_square_request_envelope(golden_dir, manifest, tile_kernel):
     st = manifest["streams"]["square_requests_1M"]
     n = st["records"]
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
@@ -204,7 +221,7 @@ def test_square_request_envelope(golden_dir, manifest):
     assert read_status(s) == (0, 2**64 - 1)
 
 
-def test_square_response_envelope(golden_dir, manifest):
+def test_square_response_envelope(golden_dir, manifest, tile_kernel):
     st = manifest["streams"]["square_responses_1M"]
     n = st["records"]
     p = GpuPacker.for_response(NUMBER, srpc_amd.RPC_SUCCESS)
@@ -216,7 +233,7 @@ def test_square_response_envelope(golden_dir, manifest):
 
 
 @pytest.mark.parametrize("bad", [0, 5, 143, 144, 145, 9999])
-def test_request_prefix_mismatch_reported(bad):
+def test_request_prefix_mismatch_reported(bad, tile_kernel):
     n = 10_000
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
     nums = np.arange(n, dtype=np.int32) - 5000
@@ -236,7 +253,7 @@ def test_request_prefix_mismatch_reported(bad):
     assert np.array_equal(back[0], nums)
 
 
-def test_truncated_wire_bounds():
+def test_truncated_wire_bounds(tile_kernel):
     n = 1000
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
     nums = np.arange(n, dtype=np.int32)

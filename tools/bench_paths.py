@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="substring filter on case names")
+    ap.add_argument("--tile-kernel", type=int, default=None, help="TILE cases: only this kernel (0 image, 1 chunk)")
     args = ap.parse_args()
 
     import numpy as np
@@ -60,11 +61,24 @@ def main():
         return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(dev)
 
     def fixed_case(name, sch, n, prefix=b"", path=None):
+        p0 = GpuPacker(sch, prefix)
+        if path:
+            p0.force_path(path)
+        if p0.path == srpc_amd.SRPC_PATH_TILE:  # both TILE kernels, image and chunk
+            for k, tag in ((0, "img"), (1, "chunk")):
+                if args.tile_kernel in (None, k):
+                    one_fixed(f"{name}_{tag}", sch, n, prefix, path, k)
+        else:
+            one_fixed(name, sch, n, prefix, path, None)
+
+    def one_fixed(name, sch, n, prefix, path, tile_kernel):
         if args.only not in name:
             return
         p = GpuPacker(sch, prefix)
         if path:
             p.force_path(path)
+        if tile_kernel is not None:
+            p.tune(tile_kernel=tile_kernel)
         rng = np.random.default_rng(1)
         cols = []
         for k in sch.kinds:
