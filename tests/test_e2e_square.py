@@ -32,6 +32,15 @@ def test_e2e_square_fallback_on_foreign_frame():
     assert r["ok"] and r["gpu"]["fallback_requests"] >= 1
 
 
+def test_e2e_square_fallback_on_foreign_frame_of_other_length():
+    """A foreign frame 7 bytes longer moves every later frame off the 57-byte
+    grid: the rest of its batch and the bytes already read for the next batch
+    are answered on the CPU, after which batching resumes."""
+    r = _run("--mode", "gpu", "--n", "50000", "--batch", "8192", "--port", "18304", "--poison", "20000",
+             "--poison-method", "Calculator_servicer::square_v2")
+    assert r["ok"] and r["gpu"]["fallback_requests"] >= 1
+
+
 @pytest.mark.slow
 def test_e2e_square_1M_reference_digest(manifest, tmp_path):
     dump = str(tmp_path / "resp.bin")

@@ -77,6 +77,7 @@ int main(int argc, char** argv) {
     uint64_t batch = 1u << 18;
     std::string mode = "gpu", port = "18090", dump;
     int64_t poison = -1;  // request index sent with an unknown method (exercises the CPU fallback)
+    std::string poison_method = "Calculator_servicer::squarX";  // same frame length as the real one
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -86,6 +87,7 @@ int main(int argc, char** argv) {
         else if (a == "--port") port = next();
         else if (a == "--dump") dump = next();
         else if (a == "--poison") poison = std::stoll(next());
+        else if (a == "--poison-method") poison_method = next();  // another length shifts every later frame
     }
     srpc::message_registry["Number"] = []() -> std::unique_ptr<Number> { return std::make_unique<Number>(); };
 
@@ -101,8 +103,7 @@ int main(int argc, char** argv) {
     for (uint64_t i = 0; i < n; ++i) {
         srpc::packer pr;
         srpc::request_t<Number> req;
-        req.set_method_name(static_cast<int64_t>(i) == poison ? "Calculator_servicer::squarX"
-                                                              : "Calculator_servicer::square");
+        req.set_method_name(static_cast<int64_t>(i) == poison ? poison_method : "Calculator_servicer::square");
         Number v;
         v.num = nums[i];
         req.set_value(std::move(v));
