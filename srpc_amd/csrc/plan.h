@@ -167,4 +167,12 @@ struct srpc_plan {
     // string schemas (SRPC_PATH_VAR)
     uint32_t nstrings = 0;
     uint32_t fixed_bytes = 0;        // prefix + fixed fields + 8 per string field
+    int var_kernel = 0;              // SRPC_TUNE_VAR_KERNEL: 0 chunk walk (default, per A/B), 1 LDS-staged tiles
+    uint32_t var_tile = 8192;        // SRPC_TUNE_VAR_TILE: staged pack output bytes per tile
+    int var_grid = 0;                // staged pack: resident workgroups (grid-stride over tiles)
 };
+
+namespace srpc_impl {
+// var.hip: size the staged VAR pack grid for the plan's current tile.
+void configure_var(srpc_plan* p);
+}  // namespace srpc_impl

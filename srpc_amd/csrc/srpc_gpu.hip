@@ -836,6 +836,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             delete p;
             return SRPC_E_HIP;
         }
+        configure_var(p);
         *out = p;
         return SRPC_OK;
     }
@@ -927,6 +928,15 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         configure_tile(p, static_cast<uint32_t>(value));
         if (int rc = configure_chunk(p)) return rc;
         if (!p->d_chunk) p->tile_kernel = 0;
+        return SRPC_OK;
+    case SRPC_TUNE_VAR_KERNEL:
+        if ((value != 0 && value != 1) || !p->has_string) return SRPC_E_INVALID;
+        p->var_kernel = value;
+        return SRPC_OK;
+    case SRPC_TUNE_VAR_TILE:
+        if (value < 4096 || value > 32768 || value % 4096 || !p->has_string) return SRPC_E_INVALID;
+        p->var_tile = static_cast<uint32_t>(value);
+        configure_var(p);
         return SRPC_OK;
     case SRPC_TUNE_TILE_KERNEL:
         if (value != 0 && value != 1) return SRPC_E_INVALID;

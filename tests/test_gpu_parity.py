@@ -43,6 +43,20 @@ def tile_kernel(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=[(0, 8192), (1, 8192), (1, 4096), (1, 32768)], ids=["walk", "staged", "staged4k", "staged32k"])
+def var_kernel(request, monkeypatch):
+    """Run a string-schema test once per VAR pack kernel / staged tile size."""
+    init = GpuPacker.__init__
+    kernel, tile = request.param
+
+    def patched(self, *a, **kw):
+        init(self, *a, **kw)
+        if not self.record_bytes:
+            self.tune(var_kernel=kernel, var_tile=tile)
+    monkeypatch.setattr(GpuPacker, "__init__", patched)
+    return request.param
+
+
 def dev(a: np.ndarray) -> "torch.Tensor":
     """numpy -> device tensor with the same bytes (16-byte aligned allocation)."""
     b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
@@ -417,7 +431,7 @@ def _rec_offsets(kinds, offs, n, prefix_len=0):
     return r
 
 
-def test_strings_reference_fixture(golden_dir):
+def test_strings_reference_fixture(golden_dir, var_kernel):
     z = np.load(os.path.join(golden_dir, "multiple_strings_in.npz"))
     kinds = MULTIPLE.kinds
     cols = [z["a1"], z["a2"], z["a3"], z["chars"]]
@@ -458,7 +472,7 @@ def _random_string_batch(kinds, n, rng, maxlen):
 @pytest.mark.parametrize("schema,maxlen,envelope", [
     ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
     ("nested", 64, "response"), ("wide", 24, "request")])
-def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
+def test_strings_random_vs_oracle(n, schema, maxlen, envelope, var_kernel):
     kinds = {"s": [oracle.STRING],
              "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
              "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
@@ -492,7 +506,7 @@ def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
 
 
 @pytest.mark.parametrize("chars_shift,offs_shift", [(0, 0), (3, 8), (15, 8), (1, 0)])
-def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift):
+def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift, var_kernel):
     """Chars columns and offset arrays at any byte / 8-byte alignment, strings
     far longer than a 4 KiB tile, and a tiny-record run (many records per tile)."""
     kinds = [oracle.INT8, oracle.STRING, oracle.INT16]
@@ -524,7 +538,7 @@ def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift):
     assert host(wire, len(want)).tobytes() == want
 
 
-def test_strings_errors():
+def test_strings_errors(var_kernel):
     kinds = [oracle.INT32, oracle.STRING]
     n = 1000
     rng = np.random.default_rng(5)

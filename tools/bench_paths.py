@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="substring filter on case names")
     ap.add_argument("--tile-kernel", type=int, default=None, help="TILE cases: only this kernel (0 image, 1 chunk)")
+    ap.add_argument("--var", default="", help="VAR cases: comma list of KERNEL:TILE pack variants "
+                    "(e.g. 0:8192,1:8192,1:16384); default: the plan's default")
     args = ap.parse_args()
 
     import numpy as np
@@ -134,20 +136,26 @@ def main():
                             dtype=torch.uint8, device=dev) for k in kinds]
         ooffs = [torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev) if k == oracle.STRING else None
                  for k in kinds]
-        p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s)
-        torch.cuda.synchronize()
         want = oracle.pack(kinds, cols, n, prefix, list(offs))
-        ok = wire[:total].cpu().numpy().tobytes() == want
         col_bytes = sum(c.nbytes for c, k in zip(cols, kinds) if k != oracle.STRING)
         str_bytes = total - n * fixed
         alg = col_bytes + str_bytes + 8 * (n + 1) * sum(k == oracle.STRING for k in kinds) + total
-        tp = timeit(lambda: p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s))
-        tu = timeit(lambda: p.unpack_var(wire, total, n, rec, outs, ooffs, scratch, sb, stream=s))
-        rows.append({"case": name, "path": "var", "records": n, "wire_bytes": total, "alg_bytes": alg,
-                     "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
-                     "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
-                     "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
-                     "parity_ok": bool(ok)})
+        variants = [tuple(int(x) for x in v.split(":")) for v in args.var.split(",") if v] or [None]
+        for var in variants:
+            label = name if var is None else f"{name}_k{var[0]}t{var[1] // 1024}"
+            if var is not None:
+                p.tune(var_kernel=var[0], var_tile=var[1])
+            wire.fill_(0)
+            p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s)
+            torch.cuda.synchronize()
+            ok = wire[:total].cpu().numpy().tobytes() == want
+            tp = timeit(lambda: p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s))
+            tu = timeit(lambda: p.unpack_var(wire, total, n, rec, outs, ooffs, scratch, sb, stream=s))
+            rows.append({"case": label, "path": "var", "records": n, "wire_bytes": total, "alg_bytes": alg,
+                         "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
+                         "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
+                         "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
+                         "parity_ok": bool(ok)})
 
     N = 1 << 24
     fixed_case("quad_dword_16M", QUAD, N)
@@ -160,6 +168,9 @@ def main():
     var_case("multiple_primitives_str0-64_4M", [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING],
              1 << 22, 64)
     var_case("string_0-1024_1M", [oracle.STRING], 1 << 20, 1024)
+    var_case("string_0-16_8M", [oracle.STRING], 1 << 23, 16)
+    var_case("two_str_request_0-32_4M", [oracle.STRING, oracle.INT32, oracle.STRING], 1 << 22, 32,
+             srpc_amd.request_prefix("Svc_servicer::method", "TwoStr"))
     txt = json.dumps(rows, indent=1)
     if args.out:
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)

@@ -10,7 +10,7 @@ from collections import defaultdict
 def short(name: str) -> str:
     m = re.search(r"(k_\w+)", name)
     base = m.group(1) if m else name[:40]
-    for tag in ("PackSizes", "ArrayVals"):
+    for tag in ("PackSizes", "ArrayVals", "FirstAndChars"):
         if tag in name:
             base += f"<{tag}>"
     return base

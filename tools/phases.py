@@ -9,6 +9,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NAMES = ["tile_first load", "window load + barrier", "find_record", "segment walk", "store", "end barrier"]
+STAGED = ["region table (lane 0)", "barrier 1", "staging loads", "barrier 2", "chunk table + barrier 3",
+          "assemble + store", "-", "end barrier"]
 
 
 def main():
@@ -38,6 +40,8 @@ def main():
     fixed = sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds)
     total = n * fixed + sum(int(o.view(torch.int64)[-1].item()) for o in offs if o is not None)
     p = GpuPacker(Schema("V", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    if os.environ.get("SRPC_PHASES_STAGED"):
+        p.tune(var_kernel=1, var_tile=int(os.environ["SRPC_PHASES_STAGED"]))
     wire = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     rec = torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev)
     sb = p.var_scratch_bytes(n, total)
@@ -56,10 +60,12 @@ def main():
     fn(h, 1)
     v = list(h)
     tiles = v[6]
-    tot = sum(v[:6])
+    names = STAGED if os.environ.get("SRPC_PHASES_STAGED") else NAMES
+    idx = [i for i, nm in enumerate(names) if nm != "-"]
+    tot = sum(v[i] for i in idx)
     print(f"tiles {tiles / reps:.0f} per call, {tot / tiles:.0f} cycles per tile (thread 0 of each workgroup)")
-    for i, nm in enumerate(NAMES):
-        print(f"   {nm:22s} {v[i] / tiles:8.0f} cyc/tile  {100 * v[i] / tot:5.1f} %")
+    for i in idx:
+        print(f"   {names[i]:24s} {v[i] / tiles:8.0f} cyc/tile  {100 * v[i] / tot:5.1f} %")
 
 
 if __name__ == "__main__":
