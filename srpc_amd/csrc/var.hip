@@ -136,8 +136,11 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* t
     return before + inc - x;
 }
 
+// Every scan kernel takes `gate`: when non-null and *gate == 0 it does nothing
+// (the single-string unpack's error path, see k_unpack_var_walk).
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_t* partial) {
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_t* partial, const uint32_t* gate) {
+    if (gate && *gate == 0) return;
     const uint64_t base = blockIdx.x * kScanBlock;
     uint64_t s = 0;
 #pragma unroll
@@ -151,7 +154,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_
 }
 
 // One workgroup: exclusive scan of nb partials in place, partial[nb] = total.
-__global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uint64_t nb) {
+__global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uint64_t nb, const uint32_t* gate) {
+    if (gate && *gate == 0) return;
     const uint64_t per = (nb + kBlock - 1) / kBlock;
     const uint64_t lo = threadIdx.x * per, hi = min(nb, lo + per);
     uint64_t s = 0;
@@ -174,7 +178,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uin
 template <class F, class M>
 __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, const uint64_t* partial, uint64_t nb,
                                                        uint64_t* out, uint64_t* tile_first, uint64_t max_tiles,
-                                                       uint64_t tile_bytes, uint32_t meta_stride) {
+                                                       uint64_t tile_bytes, uint32_t meta_stride,
+                                                       const uint32_t* gate) {
+    if (gate && *gate == 0) return;
     __shared__ uint64_t v[kScanBlock];
     const uint64_t base = blockIdx.x * kScanBlock;
 #pragma unroll
@@ -208,6 +214,24 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
         if (base + k < n) out[base + k] = v[k];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = partial[nb];
+}
+
+// Single-string schemas need no scan for the record index: record r starts at
+// (soff[r] - soff[0]) + r * fixed_bytes.  One pass writes rec_offs[0..n] and
+// the first record of every kTileBytes wire tile (what k_scan_apply<PackSizes>
+// writes for any schema).
+__global__ __launch_bounds__(kBlock) void k_single_rec_offs(const uint64_t* __restrict__ soff, uint64_t n,
+                                                            uint32_t fixed_bytes, uint64_t* __restrict__ rec_offs,
+                                                            uint64_t* __restrict__ tile_first, uint64_t max_tiles) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (r > n) return;
+    const uint64_t s0 = soff[0], sr = soff[r];
+    const uint64_t start = sr - s0 + r * fixed_bytes;
+    rec_offs[r] = start;
+    if (r == n) return;
+    const uint64_t end = soff[r + 1] - s0 + (r + 1) * fixed_bytes;
+    for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
+        tile_first[t] = r;
 }
 
 // ---- record / chunk location -------------------------------------------------
@@ -725,10 +749,26 @@ __global__ __launch_bounds__(kBlock) void k_pack_var_staged(VarArgs a, StagedLay
 // the reference checks after the read, core.hpp:29-31) or a record whose size
 // disagrees with the index is a BOUNDS error: that record's strings are
 // decoded as empty.
+//
+// Single-string schemas (soff1 != null): the string's output offset needs no
+// scan -- every record's string length is its size minus fixed_bytes, so
+// str_offs[r] = rec_offs[r] - rec_offs[0] - r * fixed_bytes -- and its chars
+// start len_at + 8 bytes into the record, so lens/spos are not written.  The
+// walk writes str_offs and the chars tiles' first records itself; a record
+// whose decoded length differs from that (any BOUNDS record, or a size
+// mismatch under a PREFIX error) sets *bad, which runs the gated scan of
+// SingleStrLen that rewrites both with the general path's semantics.
+struct SingleFast {
+    uint64_t* soff1;       // str_offs of the string field (n + 1)
+    uint64_t* tiles;       // chars tiles' first records
+    uint64_t max_tiles;
+    uint32_t* bad;
+};
+
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
                                                             uint64_t n, uint64_t* lens, uint64_t* spos,
-                                                            srpc_unpack_status* st) {
+                                                            srpc_unpack_status* st, SingleFast fast) {
     __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
     for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
     __syncthreads();
@@ -772,30 +812,71 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         } else {
             flag = SRPC_STATUS_BOUNDS;
         }
-        spos[si * n + r] = pos;
-        lens[si * n + r] = len;
+        if (!fast.soff1) {
+            spos[si * n + r] = pos;
+            lens[si * n + r] = len;
+        }
         pos += len;
     }
     if (!flag && pos != end) flag = SRPC_STATUS_BOUNDS;  // record size disagrees with the index
-    if (flag == SRPC_STATUS_BOUNDS)  // positions are untrustworthy: decode nothing of this record's strings
+    if (fast.soff1) {
+        const uint64_t first = rec_offs[0];
+        const uint64_t o = start - first - r * a.fixed_bytes;  // the output offset if every record is exact
+        fast.soff1[r] = o;
+        if (r == n - 1) fast.soff1[n] = rec_offs[n] - first - n * a.fixed_bytes;
+        // exact: the decoded length (0 for BOUNDS) is the index's size - fixed_bytes
+        const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end;
+        if (exact) {
+            const uint64_t len = end - start - a.fixed_bytes;
+            for (uint64_t t = (o + kTileBytes - 1) / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
+                fast.tiles[t] = r;
+        } else {
+            atomicOr(fast.bad, 1u);
+        }
+    } else if (flag == SRPC_STATUS_BOUNDS) {  // positions are untrustworthy: decode nothing of this record's strings
         for (uint32_t si = 0; si < a.nstrings; ++si) lens[si * n + r] = 0;
+    }
     if (flag && st) report_bad(st, flag, r);
 }
 
+// The single-string error path's lengths: exactly the length the walk
+// decodes for record r (0 for a BOUNDS record).
+struct SingleStrLen {
+    const uint8_t* wire;
+    uint64_t wire_len;
+    const uint64_t* rec;
+    const uint8_t* prefix;
+    uint32_t prefix_len, len_at, fixed_bytes;
+    __device__ uint64_t operator()(uint64_t r) const {
+        const uint64_t start = rec[r], end = rec[r + 1];
+        if (start > end || end > wire_len || end - start < fixed_bytes) return 0;
+        const uint64_t len = load_unaligned<uint64_t>(wire + start + len_at);
+        if (len > end - (start + len_at + 8)) return 0;
+        if (len == end - start - fixed_bytes) return len;
+        for (uint32_t i = 0; i < prefix_len; ++i)  // a PREFIX record keeps its length; otherwise it is BOUNDS
+            if (wire[start + i] != prefix[i]) return len;
+        return 0;
+    }
+};
+
 // Chars of one string field: output chunk c = bytes [16c, 16c+16) of chars.
+// Record r's chars start at spos[r] in the wire, or (single-string schemas,
+// spos == null) at rec_offs[r] + chars_at, staged with the window.
 __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                              const uint64_t* __restrict__ soff,
                                                              const uint64_t* __restrict__ tile_first,
                                                              const uint64_t* __restrict__ spos, uint64_t n,
-                                                             uint8_t* __restrict__ chars) {
+                                                             uint8_t* __restrict__ chars,
+                                                             const uint64_t* __restrict__ rec_offs, uint32_t chars_at) {
     __shared__ uint64_t win[kWindow];
+    __shared__ uint64_t rwin[kWindow];
     __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
         const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
-        const Window w = load_window(soff, n, r0, rz, win);
+        const Window w = spos ? load_window(soff, n, r0, rz, win) : load_window2(soff, rec_offs, n, r0, rz, win, rwin);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < total) {
             const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
@@ -808,8 +889,10 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
                 const uint64_t rs = k + 1 < w.len ? win[k] : soff[r];
                 const uint64_t re = k + 1 < w.len ? win[k + 1] : soff[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                if (cnt)
-                    put(c, wire + spos[r] + (p - rs), static_cast<int>(b), static_cast<int>(cnt), wire + wire_len);
+                if (cnt) {
+                    const uint64_t sp = spos ? spos[r] : (k + 1 < w.len ? rwin[k] : rec_offs[r]) + chars_at;
+                    put(c, wire + sp + (p - rs), static_cast<int>(b), static_cast<int>(cnt), wire + wire_len);
+                }
                 b += cnt;
                 p += cnt;
                 ++r;
@@ -820,11 +903,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
     }
 }
 
-__global__ void k_reset_status(srpc_unpack_status* st) {
+__global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad) {
     if (threadIdx.x == 0) {
-        st->flags = 0;
-        st->reserved = 0;
-        st->first_bad_record = ~0ull;
+        if (st) {
+            st->flags = 0;
+            st->reserved = 0;
+            st->first_bad_record = ~0ull;
+        }
+        if (bad) *bad = 0;
     }
 }
 
@@ -868,13 +954,14 @@ StagedLayout staged_layout(const srpc_plan* p, uint32_t T) {
 
 template <class F, class M = FirstOnly>
 int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* tile_first, uint64_t max_tiles,
-                hipStream_t s, uint64_t tile_bytes = kTileBytes, uint32_t meta_stride = 1) {
+                hipStream_t s, uint64_t tile_bytes = kTileBytes, uint32_t meta_stride = 1,
+                const uint32_t* gate = nullptr) {
     const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
     if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial);
-    launch(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb);
+    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, gate);
+    launch(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb, gate);
     launch(k_scan_apply<F, M>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, M{}, n, partial, nb, out,
-           tile_first, max_tiles, tile_bytes, meta_stride);
+           tile_first, max_tiles, tile_bytes, meta_stride, gate);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
@@ -905,7 +992,7 @@ VarArgs make_var_args(const srpc_plan* p, const void* const* cols, const uint64_
 //   unpack only: [lens: ns*n u64] [spos: ns*n u64]
 // Pack has one tile domain (the wire); unpack one per string field (its chars).
 struct ScratchLayout {
-    uint64_t partial_off, tiles_off, lens_off, spos_off, total;
+    uint64_t partial_off, tiles_off, lens_off, spos_off, bad_off, total;
     uint64_t max_tiles;
 };
 
@@ -923,7 +1010,8 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     const uint64_t domains = unpack ? p->nstrings : 1 + p->nstrings;
     L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
     L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
-    L.total = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
+    L.bad_off = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
+    L.total = L.bad_off + 256;
     return L;
 }
 
@@ -977,7 +1065,7 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
@@ -1007,9 +1095,16 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
                tiles, wire, wire_cap, st);
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
-    int rc = launch_scan(PackSizes{a}, n, partial, rec_offs, tiles, L.max_tiles, s);
-    if (rc) return rc;
-    if (n == 0) return SRPC_OK;
+    if (p->nstrings == 1) {
+        const uint64_t g1 = n / kBlock + 1;
+        if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_single_rec_offs, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a.soff[a.sfield[0]], n,
+               p->fixed_bytes, rec_offs, tiles, L.max_tiles);
+    } else {
+        int rc = launch_scan(PackSizes{a}, n, partial, rec_offs, tiles, L.max_tiles, s);
+        if (rc) return rc;
+    }
+    if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (!wire) return SRPC_E_INVALID;
     launch(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
@@ -1022,7 +1117,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
@@ -1044,10 +1139,27 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     auto* spos = reinterpret_cast<uint64_t*>(base + L.spos_off);
     const uint64_t grid = (n + kBlock - 1) / kBlock;
     if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    auto* bad = reinterpret_cast<uint32_t*>(base + L.bad_off);
+    if (p->nstrings == 1 && n) {  // single-string fast path: no scan unless a record is not exact
+        if (!wire) return SRPC_E_INVALID;
+        const uint32_t f = a.sfield[0];
+        uint32_t len_at = p->prefix_len;  // the u64 length follows the prefix and the fixed fields before it
+        for (uint32_t g = 0; g < f; ++g) len_at += p->size[g];
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, bad);
+        const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad};
+        launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, wire_len,
+               rec_offs, n, lens, spos, st, fast);
+        int rc = launch_scan(SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes},
+                             n, partial, str_offs[f], tiles, L.max_tiles, s, kTileBytes, 1, bad);
+        if (rc) return rc;
+        launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f], tiles,
+               static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8);
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
     if (n) {
         if (!wire) return SRPC_E_INVALID;
         launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
-                           wire_len, rec_offs, n, lens, spos, st);
+               wire_len, rec_offs, n, lens, spos, st, SingleFast{});
     }
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
@@ -1059,7 +1171,8 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
-               tiles + a.sidx[f] * L.max_tiles, spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]));
+               tiles + a.sidx[f] * L.max_tiles, spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]),
+               static_cast<const uint64_t*>(nullptr), 0u);
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }

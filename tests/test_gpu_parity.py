@@ -538,6 +538,35 @@ def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift, var
     assert host(wire, len(want)).tobytes() == want
 
 
+def _model_single_string(kinds, wire: bytes, n, rec, prefix: bytes):
+    """The documented unpack_var semantics for a one-string schema on bad input
+    (include/srpc_gpu.h): a BOUNDS record decodes its string as empty, a
+    PREFIX-only record keeps its length.  Returns (str_offs, chars)."""
+    fixed = len(prefix) + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds)
+    f = kinds.index(oracle.STRING)
+    len_at = len(prefix) + sum(oracle.KIND_SIZE[k] for k in kinds[:f])
+    offs, chars = [0], bytearray()
+    for r in range(n):
+        start, end = int(rec[r]), int(rec[r + 1])
+        ln = 0
+        if start <= end <= len(wire) and end - start >= fixed:
+            ln = int.from_bytes(wire[start + len_at:start + len_at + 8], "little")
+            if ln > end - (start + len_at + 8):
+                ln = 0
+            elif ln != end - start - fixed and wire[start:start + len(prefix)] == prefix:
+                ln = 0  # size disagrees with the index: BOUNDS
+            chars += wire[start + len_at + 8:start + len_at + 8 + ln]
+        offs.append(offs[-1] + ln)
+    return np.array(offs, np.uint64), bytes(chars)
+
+
+def _check_single_string(kinds, back, boffs, wire, n, rec, prefix):
+    mo, mc = _model_single_string(kinds, bytes(wire), n, rec, prefix)
+    f = kinds.index(oracle.STRING)
+    assert np.array_equal(boffs[f], mo)
+    assert back[f].tobytes() == mc
+
+
 def test_strings_errors(var_kernel):
     kinds = [oracle.INT32, oracle.STRING]
     n = 1000
@@ -550,19 +579,28 @@ def test_strings_errors(var_kernel):
     bad = 417
     pos = int(rec[bad]) + len(p.prefix) + 4
     wire[pos:pos + 8] = (10**6).to_bytes(8, "little")
-    _, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
+    back, boffs, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
     assert st == (srpc_amd.SRPC_STATUS_BOUNDS, bad)
+    _check_single_string(kinds, back, boffs, wire, n, rec, p.prefix)
     # prefix mismatch (method name) in a later record, length bug fixed
     wire[pos:pos + 8] = int(offs[1][bad + 1] - offs[1][bad]).to_bytes(8, "little")
     wire[int(rec[700]) + 9] ^= 0x40
-    back, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
+    back, boffs, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec)
     assert st == (SRPC_STATUS_PREFIX, 700)
     assert np.array_equal(back[0], cols[0])  # fields still decoded
+    _check_single_string(kinds, back, boffs, wire, n, rec, p.prefix)
     # an index that disagrees with the record sizes
     rec2 = rec.copy()
     rec2[5] += 1
-    _, _, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec2)
+    back, boffs, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec2)
     assert st[0] & srpc_amd.SRPC_STATUS_BOUNDS and st[1] == 4
+    _check_single_string(kinds, back, boffs, wire, n, rec2, p.prefix)
+    # a PREFIX record whose size also disagrees with the index keeps its length
+    rec3 = rec.copy()
+    rec3[701] += 2
+    back, boffs, st = gpu_unpack_var(p, kinds, bytes(wire), n, rec3)
+    assert st[0] & SRPC_STATUS_PREFIX and st[1] == 700
+    _check_single_string(kinds, back, boffs, wire, n, rec3, p.prefix)
     # pack into too small a buffer: bounds flagged at the first record that does not fit
     dcols = [dev(c) for c in cols]
     doffs = [None, _dev_u64(offs[1])]
