@@ -762,8 +762,67 @@ struct SingleFast {
     uint64_t* soff1;       // str_offs of the string field (n + 1)
     uint64_t* tiles;       // chars tiles' first records
     uint64_t max_tiles;
-    uint32_t* bad;
+    uint32_t* bad;         // [0] some record is not exact
+    uint8_t* chars;        // the string field's output chars
+    uint32_t* tile_long;   // per chars tile: 1 = it holds chars the walk did not copy
+    uint32_t chars_at;     // chars start this many bytes into a record
 };
+
+// A wave whose 64 strings are all at most kShortCopy bytes copies them in the
+// walk itself (one lane per string: an unaligned 16-byte load, stores of
+// exactly len bytes); only chars tiles holding bytes of other waves' strings
+// are left to k_unpack_var_chars (A/B: tools/ab_str.sh,
+// profiles/r01_var_short_copy_ab.log -- per-lane copies of mixed lengths cost
+// more than the chars kernel saves, hence the wave-uniform rule).
+#ifndef SRPC_SHORT_COPY
+#define SRPC_SHORT_COPY 32
+#endif
+constexpr uint32_t kShortCopy = SRPC_SHORT_COPY;
+
+template <typename T>
+__device__ __forceinline__ void store_unaligned(uint8_t* p, T v) {
+    __builtin_memcpy(p, &v, sizeof(T));
+}
+
+// dst[0, len) := src[0, len); src bytes at or past src_end are never read.
+__device__ __forceinline__ void copy_short(uint8_t* dst, const uint8_t* src, uint32_t len, const uint8_t* src_end) {
+    while (len) {
+        uint64_t lo = 0, hi = 0;
+        if (src + 16 <= src_end) {
+            lo = load_unaligned<uint64_t>(src);
+            hi = load_unaligned<uint64_t>(src + 8);
+        } else {
+            for (uint32_t i = 0; i < 16 && src + i < src_end; ++i)
+                (i < 8 ? lo : hi) |= static_cast<uint64_t>(src[i]) << (8 * (i & 7));
+        }
+        if (len >= 16) {
+            store_unaligned(dst, lo);
+            store_unaligned(dst + 8, hi);
+            dst += 16;
+            src += 16;
+            len -= 16;
+            continue;
+        }
+        uint32_t o = 0;
+        if (len & 8) {
+            store_unaligned(dst, lo);
+            lo = hi;
+            o = 8;
+        }
+        if (len & 4) {
+            store_unaligned(dst + o, static_cast<uint32_t>(lo));
+            lo >>= 32;
+            o += 4;
+        }
+        if (len & 2) {
+            store_unaligned(dst + o, static_cast<uint16_t>(lo));
+            lo >>= 16;
+            o += 2;
+        }
+        if (len & 1) dst[o] = static_cast<uint8_t>(lo);
+        return;
+    }
+}
 
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
@@ -826,10 +885,19 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         if (r == n - 1) fast.soff1[n] = rec_offs[n] - first - n * a.fixed_bytes;
         // exact: the decoded length (0 for BOUNDS) is the index's size - fixed_bytes
         const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end;
+        const uint64_t len = end - start - a.fixed_bytes;
+        // a wave whose strings are all short copies them here; otherwise its
+        // strings' chars tiles are left to k_unpack_var_chars
+        const bool all_short = __all(exact && len <= kShortCopy);
         if (exact) {
-            const uint64_t len = end - start - a.fixed_bytes;
             for (uint64_t t = (o + kTileBytes - 1) / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
                 fast.tiles[t] = r;
+            if (all_short) {
+                copy_short(fast.chars + o, wire + start + fast.chars_at, static_cast<uint32_t>(len), wire + wire_len);
+            } else {
+                for (uint64_t t = o / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
+                    fast.tile_long[t] = 1;
+            }
         } else {
             atomicOr(fast.bad, 1u);
         }
@@ -867,15 +935,24 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
                                                              const uint64_t* __restrict__ tile_first,
                                                              const uint64_t* __restrict__ spos, uint64_t n,
                                                              uint8_t* __restrict__ chars,
-                                                             const uint64_t* __restrict__ rec_offs, uint32_t chars_at) {
+                                                             const uint64_t* __restrict__ rec_offs, uint32_t chars_at,
+                                                             const uint32_t* __restrict__ tile_long,
+                                                             const uint32_t* __restrict__ bad) {
     __shared__ uint64_t win[kWindow];
     __shared__ uint64_t rwin[kWindow];
     __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
+    // bad[0]: some record is not exact (then every tile is copied here)
+    const bool skip_short = bad && bad[0] == 0;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        // three independent scalar loads issued together (no branch between them)
+        const uint32_t needed = tile_long[skip_short ? t : 0] | !skip_short;
+        const uint64_t r0 = tile_first[t], r1 = tile_first[min(t + 1, ntiles - 1)];
+        asm volatile("" ::"s"(r0), "s"(r1));  // keeps the tile_first loads above the branch
+        if (!needed) continue;
         const uint64_t lo = t * kTileBytes;
-        const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
+        const uint64_t rz = t + 1 < ntiles ? max(r1, r0) : n - 1;
         const Window w = spos ? load_window(soff, n, r0, rz, win) : load_window2(soff, rec_offs, n, r0, rz, win, rwin);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < total) {
@@ -910,7 +987,7 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad) {
             st->reserved = 0;
             st->first_bad_record = ~0ull;
         }
-        if (bad) *bad = 0;
+        if (bad) bad[0] = 0;
     }
 }
 
@@ -992,7 +1069,7 @@ VarArgs make_var_args(const srpc_plan* p, const void* const* cols, const uint64_
 //   unpack only: [lens: ns*n u64] [spos: ns*n u64]
 // Pack has one tile domain (the wire); unpack one per string field (its chars).
 struct ScratchLayout {
-    uint64_t partial_off, tiles_off, lens_off, spos_off, bad_off, total;
+    uint64_t partial_off, tiles_off, lens_off, spos_off, bad_off, long_off, total;
     uint64_t max_tiles;
 };
 
@@ -1011,7 +1088,8 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
     L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
     L.bad_off = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
-    L.total = L.bad_off + 256;
+    L.long_off = L.bad_off + 256;
+    L.total = L.long_off + (unpack ? round256(4 * L.max_tiles) : 0);
     return L;
 }
 
@@ -1146,14 +1224,18 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         uint32_t len_at = p->prefix_len;  // the u64 length follows the prefix and the fixed fields before it
         for (uint32_t g = 0; g < f; ++g) len_at += p->size[g];
         hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, bad);
-        const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad};
+        auto* tile_long = reinterpret_cast<uint32_t*>(base + L.long_off);
+        if (hipMemsetAsync(tile_long, 0, 4 * L.max_tiles, s) != hipSuccess) return SRPC_E_HIP;
+        const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
+                              len_at + 8};
         launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, wire_len,
                rec_offs, n, lens, spos, st, fast);
         int rc = launch_scan(SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes},
                              n, partial, str_offs[f], tiles, L.max_tiles, s, kTileBytes, 1, bad);
         if (rc) return rc;
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f], tiles,
-               static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8);
+               static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8,
+               static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad));
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     if (n) {
@@ -1172,7 +1254,8 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (p->size[f]) continue;
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],
                tiles + a.sidx[f] * L.max_tiles, spos + a.sidx[f] * n, n, static_cast<uint8_t*>(cols[f]),
-               static_cast<const uint64_t*>(nullptr), 0u);
+               static_cast<const uint64_t*>(nullptr), 0u, reinterpret_cast<const uint32_t*>(tiles),
+               static_cast<const uint32_t*>(nullptr));
     }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }

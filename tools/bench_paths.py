@@ -169,6 +169,7 @@ def main():
              1 << 22, 64)
     var_case("string_0-1024_1M", [oracle.STRING], 1 << 20, 1024)
     var_case("string_0-16_8M", [oracle.STRING], 1 << 23, 16)
+    var_case("string_0-32_4M", [oracle.STRING], 1 << 22, 32)
     var_case("two_str_request_0-32_4M", [oracle.STRING, oracle.INT32, oracle.STRING], 1 << 22, 32,
              srpc_amd.request_prefix("Svc_servicer::method", "TwoStr"))
     txt = json.dumps(rows, indent=1)
