@@ -46,6 +46,7 @@ constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 
 constexpr uint32_t kTileBytes = kBlock * 16;                                  // 4 KiB output tile
 constexpr uint32_t kWindow = 528;   // record starts staged in LDS per tile (>= 4096/8 + 2)
 constexpr int kVarGrid = 2048;      // resident workgroups for grid-stride tiles
+constexpr uint32_t kLongFlags = 256; // k_single_pack_short -> k_pack_var<true> flags, 64 bytes apart
 
 struct VarArgs {
     const uint8_t* col[kMaxFields];   // fixed: column; string: chars
@@ -214,24 +215,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
         if (base + k < n) out[base + k] = v[k];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = partial[nb];
-}
-
-// Single-string schemas need no scan for the record index: record r starts at
-// (soff[r] - soff[0]) + r * fixed_bytes.  One pass writes rec_offs[0..n] and
-// the first record of every kTileBytes wire tile (what k_scan_apply<PackSizes>
-// writes for any schema).
-__global__ __launch_bounds__(kBlock) void k_single_rec_offs(const uint64_t* __restrict__ soff, uint64_t n,
-                                                            uint32_t fixed_bytes, uint64_t* __restrict__ rec_offs,
-                                                            uint64_t* __restrict__ tile_first, uint64_t max_tiles) {
-    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (r > n) return;
-    const uint64_t s0 = soff[0], sr = soff[r];
-    const uint64_t start = sr - s0 + r * fixed_bytes;
-    rec_offs[r] = start;
-    if (r == n) return;
-    const uint64_t end = soff[r + 1] - s0 + (r + 1) * fixed_bytes;
-    for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
-        tile_first[t] = r;
 }
 
 // ---- record / chunk location -------------------------------------------------
@@ -405,10 +388,16 @@ __device__ __forceinline__ void emit_record(const VarArgs& a, const uint64_t* cl
     }
 }
 
+// kSkip (single-string schemas): return at once when k_single_pack_short
+// wrote every record.  All or nothing, and a separate instantiation: a
+// per-tile skip test in this loop, in any form, made the kernel 40 % slower
+// for every schema, even never taken (profiles/r01_var_short_copy_ab.log).
+template <bool kSkip>
 __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* __restrict__ rec_offs, uint64_t n,
                                                      const uint64_t* __restrict__ tile_first,
                                                      uint8_t* __restrict__ wire, uint64_t wire_cap,
-                                                     srpc_unpack_status* st) {
+                                                     srpc_unpack_status* st, const uint32_t* __restrict__ some_long,
+                                                     const uint64_t* __restrict__ soff0) {
     __shared__ uint64_t win[kWindow];
     __shared__ uint64_t swin[kWindow];       // char offsets of the first string field, same records
     __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
@@ -421,12 +410,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
         report_bad(st, SRPC_STATUS_BOUNDS, upper_index(rec_offs, n, wire_cap));
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
+    if constexpr (kSkip)  // k_single_pack_short wrote every record
+        if (!__syncthreads_or(threadIdx.x < kLongFlags && some_long[threadIdx.x * 16])) return;
     PHASE_BEGIN
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t lo = t * kTileBytes;
         const uint64_t r0 = tile_first[t], rz = t + 1 < ntiles ? max(tile_first[t + 1], r0) : n - 1;
         PHASE(0);
-        const Window w = load_window2(rec_offs, a.soff[f0], n, r0, rz, win, swin);
+        const Window w = load_window2(rec_offs, soff0, n, r0, rz, win, swin);
         PHASE(1);
         const uint64_t p0 = lo + 16ull * threadIdx.x;
         if (p0 < limit) {
@@ -824,6 +815,82 @@ __device__ __forceinline__ void copy_short(uint8_t* dst, const uint8_t* src, uin
     }
 }
 
+// k <= 8 low bytes of v at p (unaligned).
+__device__ __forceinline__ void store_bytes(uint8_t* p, uint64_t v, uint32_t k) {
+    if (k == 8) {
+        store_unaligned(p, v);
+        return;
+    }
+    uint32_t o = 0;
+    if (k & 4) {
+        store_unaligned(p, static_cast<uint32_t>(v));
+        v >>= 32;
+        o = 4;
+    }
+    if (k & 2) {
+        store_unaligned(p + o, static_cast<uint16_t>(v));
+        v >>= 16;
+        o += 2;
+    }
+    if (k & 1) p[o] = static_cast<uint8_t>(v);
+}
+
+// Single-string pack, before k_pack_var.  The record index needs no scan:
+// record r starts at (soff[r] - soff[0]) + r * fixed_bytes.  One record per
+// lane writes rec_offs[0..n] and the first record of every kTileBytes wire
+// tile (what k_scan_apply<PackSizes> writes for any schema).  A wave whose
+// strings are all <= kShortCopy bytes (and whose batch fits wire_cap) also
+// writes its records' wire bytes -- prefix, fixed fields, u64 length, chars --
+// with unaligned stores of exactly their bytes; any other wave sets
+// *some_long, and then k_pack_var<true> writes the whole batch again
+// (all or nothing, see k_pack_var).
+__global__ __launch_bounds__(kBlock) void k_single_pack_short(VarArgs a, uint64_t n, uint64_t* __restrict__ rec_offs,
+                                                              uint64_t* __restrict__ tile_first,
+                                                              uint32_t* __restrict__ some_long, uint64_t max_tiles,
+                                                              uint8_t* __restrict__ wire, uint64_t wire_cap) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint32_t fs = a.sfield[0];
+    const uint64_t* soff = a.soff[fs];
+    const uint64_t s0 = soff[0], sr = soff[min(r, n)];
+    const uint64_t start = sr - s0 + r * a.fixed_bytes;
+    if (r <= n) rec_offs[r] = start;
+    const uint64_t total = soff[n] - s0 + n * a.fixed_bytes;
+    const uint64_t len = r < n ? soff[r + 1] - sr : 0;
+    const uint64_t end = start + a.fixed_bytes + len;
+    if (r < n)
+        for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
+            tile_first[t] = r;
+    const bool all_short = __all(len <= kShortCopy && total <= wire_cap);
+    // some_long: kLongFlags flags 64 bytes apart, one store per long workgroup
+    // (a single flag written by every long wave serialised them: 15 -> 63 us)
+    if (__syncthreads_or(!all_short)) {
+        if (threadIdx.x == 0) some_long[(blockIdx.x % kLongFlags) * 16] = 1;
+        return;
+    }
+    if (r >= n) return;
+    uint8_t* d = wire + start;
+    for (uint32_t i = 0; i < a.prefix_len; i += 8)  // the device prefix has 16 zero bytes after it
+        store_bytes(d + i, load_unaligned<uint64_t>(a.prefix + i), min(8u, a.prefix_len - i));
+    d += a.prefix_len;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            const uint8_t* c = a.col[f] + r * sz;
+            const uint64_t v = sz == 1   ? *c
+                               : sz == 2 ? load_unaligned<uint16_t>(c)
+                               : sz == 4 ? load_unaligned<uint32_t>(c)
+                                         : load_unaligned<uint64_t>(c);
+            store_bytes(d, v, sz);
+            d += sz;
+            continue;
+        }
+        store_unaligned(d, len);
+        d += 8;
+        copy_short(d, a.col[f] + sr, static_cast<uint32_t>(len), a.col[f] + soff[n]);
+        d += len;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
                                                             uint64_t n, uint64_t* lens, uint64_t* spos,
@@ -980,15 +1047,15 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
     }
 }
 
-__global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad) {
-    if (threadIdx.x == 0) {
-        if (st) {
-            st->flags = 0;
-            st->reserved = 0;
-            st->first_bad_record = ~0ull;
-        }
-        if (bad) bad[0] = 0;
+// bad: nflags u32 flags, 64 bytes apart.
+__global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t nflags) {
+    if (threadIdx.x == 0 && st) {
+        st->flags = 0;
+        st->reserved = 0;
+        st->first_bad_record = ~0ull;
     }
+    if (bad)
+        for (uint32_t i = threadIdx.x; i < nflags; i += blockDim.x) bad[16 * i] = 0;
 }
 
 // ---- host helpers -------------------------------------------------------------
@@ -1088,8 +1155,8 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
     L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
     L.bad_off = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
-    L.long_off = L.bad_off + 256;
-    L.total = L.long_off + (unpack ? round256(4 * L.max_tiles) : 0);
+    L.long_off = L.bad_off + 64 * kLongFlags;
+    L.total = L.long_off + round256(4 * L.max_tiles);
     return L;
 }
 
@@ -1143,7 +1210,7 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr, 0u);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
@@ -1173,18 +1240,33 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
                tiles, wire, wire_cap, st);
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
+    uint32_t* some_long = nullptr;
     if (p->nstrings == 1) {
         const uint64_t g1 = n / kBlock + 1;
         if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-        launch(k_single_rec_offs, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a.soff[a.sfield[0]], n,
-               p->fixed_bytes, rec_offs, tiles, L.max_tiles);
+        if (n && !wire) return SRPC_E_INVALID;
+        some_long = reinterpret_cast<uint32_t*>(base + L.bad_off);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
+        launch(k_single_pack_short, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs, tiles,
+               some_long, L.max_tiles, wire, wire_cap);
     } else {
         int rc = launch_scan(PackSizes{a}, n, partial, rec_offs, tiles, L.max_tiles, s);
         if (rc) return rc;
     }
     if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (!wire) return SRPC_E_INVALID;
-    launch(k_pack_var, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st);
+    // soff0 = a.soff[first string field] as its own argument: indexed out of
+    // VarArgs, the compiler re-loads it from the kernarg segment inside the
+    // tile loop (a dependent scalar load per tile, +40 % kernel time,
+    // profiles/r01_var_short_copy_ab.log)
+    uint32_t f0 = 0;
+    while (p->size[f0]) ++f0;
+    if (some_long)
+        launch(k_pack_var<true>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
+               static_cast<const uint32_t*>(some_long), a.soff[f0]);
+    else
+        launch(k_pack_var<false>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
+               static_cast<const uint32_t*>(nullptr), a.soff[f0]);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
@@ -1195,7 +1277,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     if (st) {
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr, 0u);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
     if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
@@ -1223,7 +1305,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         const uint32_t f = a.sfield[0];
         uint32_t len_at = p->prefix_len;  // the u64 length follows the prefix and the fixed fields before it
         for (uint32_t g = 0; g < f; ++g) len_at += p->size[g];
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, bad);
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, bad, 1u);
         auto* tile_long = reinterpret_cast<uint32_t*>(base + L.long_off);
         if (hipMemsetAsync(tile_long, 0, 4 * L.max_tiles, s) != hipSuccess) return SRPC_E_HIP;
         const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
