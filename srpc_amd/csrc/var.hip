@@ -46,7 +46,8 @@ constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 
 constexpr uint32_t kTileBytes = kBlock * 16;                                  // 4 KiB output tile
 constexpr uint32_t kWindow = 528;   // record starts staged in LDS per tile (>= 4096/8 + 2)
 constexpr int kVarGrid = 2048;      // resident workgroups for grid-stride tiles
-constexpr uint32_t kLongFlags = 256; // k_single_pack_short -> k_pack_var<true> flags, 64 bytes apart
+constexpr uint32_t kLongFlags = 256; // k_pack_short_records -> k_pack_var<true> flags, 64 bytes apart
+constexpr uint32_t kShortRecord = 64; // records written one per lane are at most this long
 
 struct VarArgs {
     const uint8_t* col[kMaxFields];   // fixed: column; string: chars
@@ -388,8 +389,7 @@ __device__ __forceinline__ void emit_record(const VarArgs& a, const uint64_t* cl
     }
 }
 
-// kSkip (single-string schemas): return at once when k_single_pack_short
-// wrote every record.  All or nothing, and a separate instantiation: a
+// kSkip: return at once when k_pack_short_records wrote every record.  All or nothing, and a separate instantiation: a
 // per-tile skip test in this loop, in any form, made the kernel 40 % slower
 // for every schema, even never taken (profiles/r01_var_short_copy_ab.log).
 template <bool kSkip>
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
         report_bad(st, SRPC_STATUS_BOUNDS, upper_index(rec_offs, n, wire_cap));
     const uint64_t ntiles = (limit + kTileBytes - 1) / kTileBytes;
-    if constexpr (kSkip)  // k_single_pack_short wrote every record
+    if constexpr (kSkip)  // k_pack_short_records wrote every record
         if (!__syncthreads_or(threadIdx.x < kLongFlags && some_long[threadIdx.x * 16])) return;
     PHASE_BEGIN
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -835,32 +835,47 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, uint64_t v, uint32_t k) 
     if (k & 1) p[o] = static_cast<uint8_t>(v);
 }
 
-// Single-string pack, before k_pack_var.  The record index needs no scan:
-// record r starts at (soff[r] - soff[0]) + r * fixed_bytes.  One record per
-// lane writes rec_offs[0..n] and the first record of every kTileBytes wire
-// tile (what k_scan_apply<PackSizes> writes for any schema).  A wave whose
-// strings are all <= kShortCopy bytes (and whose batch fits wire_cap) also
-// writes its records' wire bytes -- prefix, fixed fields, u64 length, chars --
-// with unaligned stores of exactly their bytes; any other wave sets
-// *some_long, and then k_pack_var<true> writes the whole batch again
-// (all or nothing, see k_pack_var).
-__global__ __launch_bounds__(kBlock) void k_single_pack_short(VarArgs a, uint64_t n, uint64_t* __restrict__ rec_offs,
-                                                              uint64_t* __restrict__ tile_first,
-                                                              uint32_t* __restrict__ some_long, uint64_t max_tiles,
-                                                              uint8_t* __restrict__ wire, uint64_t wire_cap) {
+// Pack, before k_pack_var, one record per lane.  Single-string schemas
+// (kSingle) need no scan for the record index: record r starts at
+// (soff[r] - soff[0]) + r * fixed_bytes, and this kernel writes rec_offs[0..n]
+// and the first record of every kTileBytes wire tile (what
+// k_scan_apply<PackSizes> writes for other schemas, which run it first).  A
+// wave whose strings are all <= kShortCopy bytes (when the batch fits
+// wire_cap; the host passes wire_cap 0 for schemas whose records can exceed
+// kShortRecord bytes) also writes its records' wire bytes -- prefix, fixed fields, u64
+// lengths, chars -- with unaligned stores of exactly their bytes; any other
+// wave sets *some_long, and then k_pack_var<true> writes the whole batch
+// again (all or nothing, see k_pack_var).
+template <bool kSingle>
+__global__ __launch_bounds__(kBlock) void k_pack_short_records(VarArgs a, uint64_t n, uint64_t* __restrict__ rec_offs,
+                                                               uint64_t* __restrict__ tile_first,
+                                                               uint32_t* __restrict__ some_long, uint64_t max_tiles,
+                                                               uint8_t* __restrict__ wire, uint64_t wire_cap) {
     const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    const uint32_t fs = a.sfield[0];
-    const uint64_t* soff = a.soff[fs];
-    const uint64_t s0 = soff[0], sr = soff[min(r, n)];
-    const uint64_t start = sr - s0 + r * a.fixed_bytes;
-    if (r <= n) rec_offs[r] = start;
-    const uint64_t total = soff[n] - s0 + n * a.fixed_bytes;
-    const uint64_t len = r < n ? soff[r + 1] - sr : 0;
-    const uint64_t end = start + a.fixed_bytes + len;
-    if (r < n)
-        for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
-            tile_first[t] = r;
-    const bool all_short = __all(len <= kShortCopy && total <= wire_cap);
+    uint64_t start, total;
+    bool short_ok = true;
+    if constexpr (kSingle) {
+        const uint64_t* soff = a.soff[a.sfield[0]];
+        const uint64_t s0 = soff[0], sr = soff[min(r, n)];
+        start = sr - s0 + r * a.fixed_bytes;
+        if (r <= n) rec_offs[r] = start;
+        total = soff[n] - s0 + n * a.fixed_bytes;
+        const uint64_t len = r < n ? soff[r + 1] - sr : 0;
+        const uint64_t end = start + a.fixed_bytes + len;
+        if (r < n)
+            for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
+                tile_first[t] = r;
+        short_ok = len <= kShortCopy;
+    } else {
+        start = rec_offs[min(r, n)];
+        total = rec_offs[n];
+        if (r < n)
+            for (uint32_t si = 0; si < a.nstrings; ++si) {
+                const uint64_t* so = a.soff[a.sfield[si]];
+                short_ok &= so[r + 1] - so[r] <= kShortCopy;
+            }
+    }
+    const bool all_short = __all(short_ok && total <= wire_cap);
     // some_long: kLongFlags flags 64 bytes apart, one store per long workgroup
     // (a single flag written by every long wave serialised them: 15 -> 63 us)
     if (__syncthreads_or(!all_short)) {
@@ -884,9 +899,11 @@ __global__ __launch_bounds__(kBlock) void k_single_pack_short(VarArgs a, uint64_
             d += sz;
             continue;
         }
+        const uint64_t* so = a.soff[f];
+        const uint64_t s = so[r], len = so[r + 1] - s;
         store_unaligned(d, len);
         d += 8;
-        copy_short(d, a.col[f] + sr, static_cast<uint32_t>(len), a.col[f] + soff[n]);
+        copy_short(d, a.col[f] + s, static_cast<uint32_t>(len), a.col[f] + so[n]);
         d += len;
     }
 }
@@ -1046,6 +1063,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
         __syncthreads();
     }
 }
+
+__global__ void k_set_flag(uint32_t* f) { *f = 1; }
 
 // bad: nflags u32 flags, 64 bytes apart.
 __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t nflags) {
@@ -1240,18 +1259,26 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
                tiles, wire, wire_cap, st);
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
-    uint32_t* some_long = nullptr;
+    const uint64_t g1 = n / kBlock + 1;
+    if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    if (n && !wire) return SRPC_E_INVALID;
+    uint32_t* some_long = reinterpret_cast<uint32_t*>(base + L.bad_off);
+    hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
+    // records that may be written one per lane: small ones only (wide per-lane
+    // records write partial cache lines: 94-byte records took 723 us against
+    // the walk's 313, profiles/r01_var_pack_short_ab.log)
+    const bool small = p->fixed_bytes + p->nstrings * kShortCopy <= kShortRecord;
     if (p->nstrings == 1) {
-        const uint64_t g1 = n / kBlock + 1;
-        if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-        if (n && !wire) return SRPC_E_INVALID;
-        some_long = reinterpret_cast<uint32_t*>(base + L.bad_off);
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
-        launch(k_single_pack_short, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs, tiles,
-               some_long, L.max_tiles, wire, wire_cap);
+        launch(k_pack_short_records<true>, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs,
+               tiles, some_long, L.max_tiles, wire, small ? wire_cap : 0);
     } else {
         int rc = launch_scan(PackSizes{a}, n, partial, rec_offs, tiles, L.max_tiles, s);
         if (rc) return rc;
+        if (n && small)
+            launch(k_pack_short_records<false>, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs,
+                   tiles, some_long, L.max_tiles, wire, wire_cap);
+        else
+            hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, s, some_long);
     }
     if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (!wire) return SRPC_E_INVALID;
@@ -1261,12 +1288,8 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     // profiles/r01_var_short_copy_ab.log)
     uint32_t f0 = 0;
     while (p->size[f0]) ++f0;
-    if (some_long)
-        launch(k_pack_var<true>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
-               static_cast<const uint32_t*>(some_long), a.soff[f0]);
-    else
-        launch(k_pack_var<false>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
-               static_cast<const uint32_t*>(nullptr), a.soff[f0]);
+    launch(k_pack_var<true>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
+           static_cast<const uint32_t*>(some_long), a.soff[f0]);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
