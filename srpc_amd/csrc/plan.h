@@ -155,6 +155,7 @@ struct srpc_plan {
     int path = 0;
     uint32_t tile_R = 0, tile_L = 0;
     int tile_grid = 0;               // resident workgroups for grid-stride tiles
+    bool tile_full_grid = true;      // image kernels: one workgroup per tile
     size_t tile_lds = 0;
     int tile_kernel = 0;             // SRPC_TUNE_TILE_KERNEL: 0 LDS image, 1 register-assembled chunks
     uint8_t* d_chunk = nullptr;      // CHUNK table blob (ChunkArgs::table), nullptr = not eligible

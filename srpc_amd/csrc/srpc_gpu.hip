@@ -335,7 +335,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __res
                 v = and_not_or(v, *reinterpret_cast<const uint4*>(mask + ph),
                                *reinterpret_cast<const uint4*>(tmpl + ph));
             }
-            *reinterpret_cast<uint4*>(dst + 16 * c) = v;
+            // non-temporal: the wire is written once (Quad on TILE 112 -> 93 us
+            // with the full grid, r01_tile_grid_nt_ab.log)
+            __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + 16 * c));
         }
         if (threadIdx.x == 0) {
             for (uint32_t i = full * 16; i < tbytes; ++i) {
@@ -422,7 +424,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
                 default: q = gather_chunk<8>(img, e0, ne, a.stride, a.off[f]); break;
                 }
                 if ((c + 1) * 16 <= nbytes) {
-                    *reinterpret_cast<uint4*>(dstc + 16 * c) = q;
+                    // non-temporal: Quad on TILE 99 -> 79 us (r01_tile_unpack_nt_ab.log)
+                    __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w}, reinterpret_cast<u32x4*>(dstc + 16 * c));
                 } else {  // the column's last, partial chunk: whole elements, bytewise from the image
                     for (uint32_t e = e0; e < nr; ++e)
                         for (uint32_t i = 0; i < s; ++i) dstc[e * s + i] = img[e * a.stride + a.off[f] + i];
@@ -653,6 +656,12 @@ void configure_tile(srpc_plan* p, uint32_t target) {
         cus = 256;
     }
     p->tile_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
+    // Image kernels: one workgroup per tile beat a resident grid-stride grid
+    // on every TILE schema (square request unpack 193 -> 167 us, response
+    // 78 -> 70 us; profiles/r01_tile_grid_nt_ab.log).  A grid-stride variant
+    // that issued the next tile's loads before draining the current image
+    // (kept in flight across the tile loop) lost to both (r01_tile_pipe_ab.log).
+    p->tile_full_grid = true;
 }
 
 // CHUNK kernel table for the current tile geometry (chunk.hip): per phase of
@@ -973,7 +982,7 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     const TileArgs a = make_tile_args(p, cols);
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     launch(k_pack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n, ntiles);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
@@ -1024,7 +1033,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         return ret;
     }
     const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols));
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_grid));
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     launch(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     return ret;

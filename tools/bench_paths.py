@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="substring filter on case names")
-    ap.add_argument("--tile-kernel", type=int, default=None, help="TILE cases: only this kernel (0 image, 1 chunk)")
+    ap.add_argument("--tile-kernel", default="0,1",
+                    help="TILE cases: comma list of kernels (0 image, 1 chunk)")
     ap.add_argument("--var", default="", help="VAR cases: comma list of KERNEL:TILE pack variants "
                     "(e.g. 0:8192,1:8192,1:16384); default: the plan's default")
     args = ap.parse_args()
@@ -66,9 +67,10 @@ def main():
         p0 = GpuPacker(sch, prefix)
         if path:
             p0.force_path(path)
-        if p0.path == srpc_amd.SRPC_PATH_TILE:  # both TILE kernels, image and chunk
+        if p0.path == srpc_amd.SRPC_PATH_TILE:  # every TILE kernel asked for
+            kernels = [int(k) for k in args.tile_kernel.split(",") if k]
             for k, tag in ((0, "img"), (1, "chunk")):
-                if args.tile_kernel in (None, k):
+                if k in kernels:
                     one_fixed(f"{name}_{tag}", sch, n, prefix, path, k)
         else:
             one_fixed(name, sch, n, prefix, path, None)
