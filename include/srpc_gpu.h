@@ -123,7 +123,8 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_ITER 2             /* records (or quads) per lane per launch: 1,2,4,8 */
 #define SRPC_TUNE_NONTEMPORAL 3      /* bit0 non-temporal stores, bit1 loads      */
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
-                                        (1024..49152)                            */
+                                        (1024..49152), pack and unpack           */
+#define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
 #define SRPC_TUNE_TILE_KERNEL 6      /* TILE path kernel: 0 = LDS image (stride-S
                                         scatter/gather), 1 = register-assembled
                                         16-byte chunks from aligned column slabs */

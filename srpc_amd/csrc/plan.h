@@ -149,6 +149,7 @@ struct srpc_plan {
     uint8_t h_prefix[srpc_impl::kMaxPrefix] = {};
     uint8_t* d_prefix = nullptr;       // device copy (d_prefix_alloc + 16, zero-padded 16 B each side)
     uint8_t* d_prefix_alloc = nullptr;
+    uint8_t* d_period = nullptr;     // TILE: template | mask of one period lcm(stride, 16) (prefixed schemas)
     uint64_t stride = 0;             // fixed record bytes (0 for string schemas)
     bool has_string = false;
     bool dword_ok = false;
@@ -156,6 +157,9 @@ struct srpc_plan {
     uint32_t tile_R = 0, tile_L = 0;
     int tile_grid = 0;               // resident workgroups for grid-stride tiles
     bool tile_full_grid = true;      // image kernels: one workgroup per tile
+    int tile_lb = 8;                 // pack image kernel: 16-byte column loads in flight per lane
+    uint32_t ptile_R = 0;            // pack image kernel: records per tile
+    size_t ptile_lds = 0;
     size_t tile_lds = 0;
     int tile_kernel = 0;             // SRPC_TUNE_TILE_KERNEL: 0 LDS image, 1 register-assembled chunks
     uint8_t* d_chunk = nullptr;      // CHUNK table blob (ChunkArgs::table), nullptr = not eligible

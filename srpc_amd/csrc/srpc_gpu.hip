@@ -55,7 +55,7 @@ struct TileArgs {
     uint32_t size[kMaxFields];       // field bytes: 1, 2, 4 or 8
     uint32_t lgsize[kMaxFields];     // log2(size)
     uint32_t off[kMaxFields];        // field byte offset inside the record (prefix included)
-    const uint8_t* prefix;           // device copy of the constant header
+    const uint8_t* period;           // device template | mask of one period (2L bytes; prefix_len > 0)
     uint32_t nfields;
     uint32_t stride;                 // record bytes
     uint32_t prefix_len;
@@ -244,13 +244,12 @@ __global__ __launch_bounds__(kBlock) void k_unpack_dword_x4(DwordMap m, const ui
 constexpr int kLoadBatch = 8;
 
 // LDS layout (dynamic, 16-byte aligned base): image[R*stride] | tmpl[L] | mask[L]
-__device__ __forceinline__ void build_template(const TileArgs& a, uint8_t* tmpl, uint8_t* mask) {
-    for (uint32_t i = threadIdx.x; i < a.L; i += kBlock) {
-        const uint32_t pos = i % a.stride;
-        const bool pre = pos < a.prefix_len;
-        tmpl[i] = pre ? a.prefix[pos] : 0;
-        mask[i] = pre ? 0xFF : 0;
-    }
+// The template and mask of one period are built once per plan in device
+// memory (plan.d_period); each workgroup copies them with 16-byte loads.
+__device__ __forceinline__ void build_template(const TileArgs& a, uint8_t* tmpl, uint8_t*) {
+    const uint32_t nch = (2 * a.L) >> 4;
+    for (uint32_t i = threadIdx.x; i < nch; i += kBlock)
+        reinterpret_cast<uint4*>(tmpl)[i] = reinterpret_cast<const uint4*>(a.period)[i];
 }
 
 __device__ __forceinline__ uint4 and_not_or(uint4 v, uint4 m, uint4 t) {
@@ -278,6 +277,9 @@ __device__ __forceinline__ uint4 gather_chunk(const uint8_t* img, uint32_t e0, u
     return q;
 }
 
+// LB: 16-byte column loads in flight per lane (the host sizes it to the
+// tile: fewer slots, fewer VGPRs, more resident workgroups).
+template <int LB>
 __global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __restrict__ wire, uint64_t n,
                                                       uint64_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -296,15 +298,15 @@ __global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __res
             const uint8_t* src = a.col[f] + rbase * s;
             const uint32_t nbytes = nr * s;
             const uint32_t nchunks = (nbytes + 15) >> 4;
-            for (uint32_t c0 = threadIdx.x; c0 < nchunks; c0 += kBlock * kLoadBatch) {
-                uint4 qq[kLoadBatch];
+            for (uint32_t c0 = threadIdx.x; c0 < nchunks; c0 += kBlock * LB) {
+                uint4 qq[LB];
 #pragma unroll
-                for (int u = 0; u < kLoadBatch; ++u) {
+                for (int u = 0; u < LB; ++u) {
                     const uint32_t c = c0 + u * kBlock;
                     if ((c + 1) * 16 <= nbytes) qq[u] = *reinterpret_cast<const uint4*>(src + 16 * c);
                 }
 #pragma unroll
-                for (int u = 0; u < kLoadBatch; ++u) {
+                for (int u = 0; u < LB; ++u) {
                     const uint32_t c = c0 + u * kBlock;
                     if (c >= nchunks) break;
                     const uint32_t e0 = (16 * c) >> lg;
@@ -581,7 +583,7 @@ DwordMap make_dword_map(const srpc_plan* p, const void* const* cols) {
     return m;
 }
 
-TileArgs make_tile_args(const srpc_plan* p, const void* const* cols) {
+TileArgs make_tile_args(const srpc_plan* p, const void* const* cols, bool pack) {
     TileArgs a{};
     for (uint32_t f = 0; f < p->nfields; ++f) {
         a.col[f] = static_cast<const uint8_t*>(cols[f]);
@@ -589,11 +591,11 @@ TileArgs make_tile_args(const srpc_plan* p, const void* const* cols) {
         a.lgsize[f] = ilog2(p->size[f]);
         a.off[f] = p->off[f];
     }
-    a.prefix = p->d_prefix;
+    a.period = p->d_period;
     a.nfields = p->nfields;
     a.stride = static_cast<uint32_t>(p->stride);
     a.prefix_len = p->prefix_len;
-    a.R = p->tile_R;
+    a.R = pack ? p->ptile_R : p->tile_R;
     a.L = p->tile_L;
     return a;
 }
@@ -642,15 +644,50 @@ DwordVariant default_dword_variant(uint32_t W) {
 // span is 16-byte aligned) with an image of about `target` bytes, the
 // template period L = lcm(stride, 16), and a grid-stride grid of as many
 // workgroups as can be resident.
+int upload_period(srpc_plan* p) {
+    if (!p->prefix_len || p->d_period) return SRPC_OK;
+    const uint32_t L = p->tile_L, S = static_cast<uint32_t>(p->stride);
+    std::vector<uint8_t> h(2 * static_cast<size_t>(L), 0);
+    for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t pos = i % S;
+        if (pos < p->prefix_len) {
+            h[i] = p->h_prefix[pos];
+            h[L + i] = 0xFF;
+        }
+    }
+    DeviceGuard g(p->device);
+    if (hipMalloc(&p->d_period, h.size()) != hipSuccess) {
+        p->d_period = nullptr;
+        return SRPC_E_HIP;
+    }
+    if (hipMemcpy(p->d_period, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) return SRPC_E_HIP;
+    return SRPC_OK;
+}
+
+// The pack image kernel's own tile (its best size differs from unpack's:
+// profiles/r01_sweep_tile.log) and its column load slots per lane, sized to
+// the widest field's slice of a tile (fewer slots, fewer VGPRs, more
+// resident workgroups).
+void configure_pack_tile(srpc_plan* p, uint32_t target) {
+    const uint32_t S = static_cast<uint32_t>(p->stride);
+    const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
+    p->ptile_R = R;
+    p->ptile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
+    uint32_t maxc = 1;
+    for (uint32_t f = 0; f < p->nfields; ++f) maxc = std::max(maxc, (R * p->size[f] + 15) / 16);
+    p->tile_lb = maxc <= kBlock ? 1 : maxc <= 2 * kBlock ? 2 : maxc <= 4 * kBlock ? 4 : 8;
+}
+
 void configure_tile(srpc_plan* p, uint32_t target) {
     const uint32_t S = static_cast<uint32_t>(p->stride);
     const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
     p->tile_R = R;
     p->tile_L = S / gcd_u32(S, 16) * 16;
     p->tile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
+    configure_pack_tile(p, target);
     int per_cu = 0, cus = 0;
     DeviceGuard g(p->device);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_tile, kBlock, p->tile_lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_tile<8>, kBlock, p->tile_lds) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) {
         per_cu = 4;
         cus = 256;
@@ -863,10 +900,20 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         return SRPC_E_HIP;
     }
     if (p->dword_ok) p->dv = default_dword_variant(static_cast<uint32_t>(o / 4));
-    // TILE image size: 32 KiB, the best or within 3 % of the best of 4-48 KiB
-    // for every record width swept on MI355X (profiles/r01_sweep_tile.log).
+    // TILE unpack image: 32 KiB, within 3 % of the best of 4-32 KiB for every
+    // record width swept on MI355X (profiles/r01_sweep_tile.log).
     if (o <= kMaxTileStride) {
         configure_tile(p, 32768);
+        // pack image: 24 KiB tiles for enveloped records, 16 KiB otherwise --
+        // the best or within 2 % of it with the columns cache-resident (pack
+        // after pack) and cold (pack after an unpack that streamed the wire
+        // through the caches) for the square request/response and Quad
+        // (profiles/r01_ab_pack_tile.log, r01_sweep_tile.log)
+        configure_pack_tile(p, p->prefix_len ? 24576 : 16384);
+        if (upload_period(p) != SRPC_OK) {
+            (void)srpc_plan_destroy(p);
+            return SRPC_E_HIP;
+        }
         if (configure_chunk(p) != SRPC_OK) {
             (void)srpc_plan_destroy(p);
             return SRPC_E_HIP;
@@ -884,6 +931,10 @@ int srpc_plan_destroy(srpc_plan* p) {
         (void)hipFree(p->d_prefix_alloc);
     }
     free_chunk(p);
+    if (p->d_period) {
+        DeviceGuard g(p->device);
+        (void)hipFree(p->d_period);
+    }
     delete p;
     return SRPC_OK;
 }
@@ -938,6 +989,10 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         if (int rc = configure_chunk(p)) return rc;
         if (!p->d_chunk) p->tile_kernel = 0;
         return SRPC_OK;
+    case SRPC_TUNE_PACK_TILE_BYTES:
+        if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
+        configure_pack_tile(p, static_cast<uint32_t>(value));
+        return SRPC_OK;
     case SRPC_TUNE_VAR_KERNEL:
         if ((value != 0 && value != 1) || !p->has_string) return SRPC_E_INVALID;
         p->var_kernel = value;
@@ -981,9 +1036,16 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
         launch(k_pack_chunk, dim3(grid), dim3(kBlock), static_cast<uint32_t>(p->chunk_lds), s, c, wire, n, ntiles);
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
-    const TileArgs a = make_tile_args(p, cols);
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
-    launch(k_pack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n, ntiles);
+    const TileArgs a = make_tile_args(p, cols, true);
+    const uint64_t ptiles = (n + p->ptile_R - 1) / p->ptile_R;
+    const uint32_t pgrid = static_cast<uint32_t>(std::min<uint64_t>(ptiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
+    const size_t lds = p->ptile_lds;
+    switch (p->tile_lb) {
+    case 1: launch(k_pack_tile<1>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 2: launch(k_pack_tile<2>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 4: launch(k_pack_tile<4>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    default: launch(k_pack_tile<8>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    }
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
@@ -1032,7 +1094,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
         return ret;
     }
-    const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols));
+    const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     launch(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;

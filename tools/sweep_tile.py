@@ -39,7 +39,7 @@ def main():
                                   ("e", "int32"), ("f", "int64")), b""),
         "quad16_tile": (QUAD, b""),
     }
-    sizes = [4096, 8192, 16384, 32768, 49152]
+    sizes = [4096, 6144, 8192, 12288, 16384, 24576, 32768]
     res = {}
     for name, (sch, pre) in cases.items():
         p = GpuPacker(sch, pre)
