@@ -45,7 +45,10 @@ constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 2048 items
 constexpr uint32_t kTileBytes = kBlock * 16;                                  // 4 KiB output tile
 constexpr uint32_t kWindow = 528;   // record starts staged in LDS per tile (>= 4096/8 + 2)
-constexpr int kVarGrid = 2048;      // resident workgroups for grid-stride tiles
+#ifndef SRPC_VAR_GRID
+#define SRPC_VAR_GRID 2048  // 8192 / 32768 within +-5 % (profiles/r01_var_grid_ab.log)
+#endif
+constexpr int kVarGrid = SRPC_VAR_GRID;  // workgroups for grid-stride tiles
 constexpr uint32_t kLongFlags = 256; // k_pack_short_records -> k_pack_var<true> flags, 64 bytes apart
 constexpr uint32_t kShortRecord = 64; // records written one per lane are at most this long
 
