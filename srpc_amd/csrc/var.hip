@@ -760,6 +760,7 @@ struct SingleFast {
     uint8_t* chars;        // the string field's output chars
     uint32_t* tile_long;   // per chars tile: 1 = it holds chars the walk did not copy
     uint32_t chars_at;     // chars start this many bytes into a record
+    uint64_t first, last;  // rec_offs[0], rec_offs[n] (set by the walk)
 };
 
 // A wave whose 64 strings are all at most kShortCopy bytes copies them in the
@@ -911,24 +912,22 @@ __global__ __launch_bounds__(kBlock) void k_pack_short_records(VarArgs a, uint64
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
-                                                            uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
-                                                            uint64_t n, uint64_t* lens, uint64_t* spos,
-                                                            srpc_unpack_status* st, SingleFast fast) {
-    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
-    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
-    __syncthreads();
-    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t start = rec_offs[r], end = rec_offs[r + 1];
+// The walk's per-record parse.  src points at the record's first wire byte
+// (in the LDS stage or in global memory), src_end bounds what may be read
+// from it; positions are wire offsets (pos - start indexes src).
+template <typename Pre>
+__device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src, const uint8_t* src_end,
+                                            const Pre* pre, uint64_t r, uint64_t start, uint64_t end,
+                                            uint64_t wire_len, uint64_t n, uint64_t* lens, uint64_t* spos,
+                                            srpc_unpack_status* st, const SingleFast& fast) {
     uint32_t flag = 0;
     if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
     if (!flag) {
         uint32_t i = 0;
         for (; i + 8 <= a.prefix_len; i += 8)
-            if (load_unaligned<uint64_t>(wire + start + i) != load_unaligned<uint64_t>(pre + i)) flag = SRPC_STATUS_PREFIX;
+            if (load_unaligned<uint64_t>(src + i) != load_unaligned<uint64_t>(pre + i)) flag = SRPC_STATUS_PREFIX;
         for (; i < a.prefix_len; ++i)
-            if (wire[start + i] != pre[i]) flag = SRPC_STATUS_PREFIX;
+            if (src[i] != pre[i]) flag = SRPC_STATUS_PREFIX;
     }
     uint64_t pos = start + a.prefix_len;
     for (uint32_t f = 0; f < a.nfields; ++f) {
@@ -936,11 +935,12 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         if (sz) {
             if (flag != SRPC_STATUS_BOUNDS) {
                 uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
+                const uint8_t* q = src + (pos - start);
                 switch (sz) {
-                case 1: dst[0] = wire[pos]; break;
-                case 2: *reinterpret_cast<uint16_t*>(dst) = load_unaligned<uint16_t>(wire + pos); break;
-                case 4: *reinterpret_cast<uint32_t*>(dst) = load_unaligned<uint32_t>(wire + pos); break;
-                default: *reinterpret_cast<uint64_t*>(dst) = load_unaligned<uint64_t>(wire + pos); break;
+                case 1: dst[0] = q[0]; break;
+                case 2: *reinterpret_cast<uint16_t*>(dst) = load_unaligned<uint16_t>(q); break;
+                case 4: *reinterpret_cast<uint32_t*>(dst) = load_unaligned<uint32_t>(q); break;
+                default: *reinterpret_cast<uint64_t*>(dst) = load_unaligned<uint64_t>(q); break;
                 }
             }
             pos += sz;
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         const uint32_t si = a.sidx[f];
         uint64_t len = 0;
         if (flag != SRPC_STATUS_BOUNDS && pos + 8 <= end) {
-            len = load_unaligned<uint64_t>(wire + pos);
+            len = load_unaligned<uint64_t>(src + (pos - start));
             pos += 8;
             if (len > end - pos) {
                 flag = SRPC_STATUS_BOUNDS;
@@ -966,10 +966,10 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
     }
     if (!flag && pos != end) flag = SRPC_STATUS_BOUNDS;  // record size disagrees with the index
     if (fast.soff1) {
-        const uint64_t first = rec_offs[0];
+        const uint64_t first = fast.first;
         const uint64_t o = start - first - r * a.fixed_bytes;  // the output offset if every record is exact
         fast.soff1[r] = o;
-        if (r == n - 1) fast.soff1[n] = rec_offs[n] - first - n * a.fixed_bytes;
+        if (r == n - 1) fast.soff1[n] = fast.last - first - n * a.fixed_bytes;
         // exact: the decoded length (0 for BOUNDS) is the index's size - fixed_bytes
         const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end;
         const uint64_t len = end - start - a.fixed_bytes;
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
             for (uint64_t t = (o + kTileBytes - 1) / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
                 fast.tiles[t] = r;
             if (all_short) {
-                copy_short(fast.chars + o, wire + start + fast.chars_at, static_cast<uint32_t>(len), wire + wire_len);
+                copy_short(fast.chars + o, src + fast.chars_at, static_cast<uint32_t>(len), src_end);
             } else {
                 for (uint64_t t = o / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
                     fast.tile_long[t] = 1;
@@ -992,6 +992,66 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         for (uint32_t si = 0; si < a.nstrings; ++si) lens[si * n + r] = 0;
     }
     if (flag && st) report_bad(st, flag, r);
+}
+
+// One record per lane.  The workgroup's 256 records are normally one
+// contiguous wire span [rec_offs[r0], rec_offs[r0 + 256]); when it fits the
+// LDS stage it is copied there first with coalesced 16-byte loads, so the
+// per-record parse (prefix, fixed fields, a chain of dependent string
+// lengths) reads LDS instead of paying an HBM round trip per length.  A
+// record outside the staged span (a long span, or an index that is not
+// monotonic) is parsed from global memory with the same code.
+constexpr uint64_t kWalkStageMax = 49152;
+
+// STAGED (multi-string schemas whose average span fits, chosen by the host):
+// the stage is dynamic LDS of stage_bytes.  Single-string schemas walk from
+// global memory: one length per record, and the LDS stage costs them more in
+// occupancy than it saves (0-16 B strings 105 -> 139 us staged).
+template <bool STAGED>
+__global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
+                                                            uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
+                                                            uint64_t n, uint64_t* lens, uint64_t* spos,
+                                                            srpc_unpack_status* st, SingleFast fast,
+                                                            uint32_t stage_bytes) {
+    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
+    const uint64_t rA = static_cast<uint64_t>(blockIdx.x) * kBlock;
+    const uint64_t rB = min<uint64_t>(rA + kBlock, n);
+    const uint64_t lo = rec_offs[rA], hi = min(rec_offs[rB], wire_len);
+    const uint64_t base = lo & ~15ull;
+    // 16 bytes past the span: a fixed field after a string may be read up to
+    // 7 bytes past its record's end (the record is then BOUNDS), as in global
+    const uint64_t shi = min(hi + 16, wire_len);
+    const bool staged = STAGED && lo < hi && shi - base <= stage_bytes;  // workgroup-uniform
+    if (staged) {
+        const uint32_t nch = static_cast<uint32_t>((shi - base + 15) >> 4);
+        for (uint32_t c = threadIdx.x; c < nch; c += kBlock) {
+            const uint64_t g = base + 16ull * c;
+            if (g + 16 <= wire_len) {
+                *reinterpret_cast<u64x2*>(stage + 16 * c) = *reinterpret_cast<const u64x2*>(wire + g);
+            } else {
+                for (uint32_t k = 0; k < 16 && g + k < wire_len; ++k) stage[16 * c + k] = wire[g + k];
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t r = rA + threadIdx.x;
+    const bool valid = r < n;
+    const uint64_t start = valid ? rec_offs[r] : 0, end = valid ? rec_offs[r + 1] : 0;
+    if (fast.soff1) {
+        fast.first = rec_offs[0];
+        fast.last = rec_offs[n];
+    }
+    // (walk_record's all-short vote then runs per branch: it only chooses
+    // between a lane copying its own string and flagging its chars tiles,
+    // and either is correct per lane)
+    if (staged && valid && start >= lo && end <= hi && start <= end) {
+        walk_record(a, stage + (start - base), stage + (shi - base), pre, r, start, end, wire_len, n, lens, spos,
+                    st, fast);
+    } else if (valid) {
+        walk_record(a, wire + start, wire + wire_len, pre, r, start, end, wire_len, n, lens, spos, st, fast);
+    }
 }
 
 // The single-string error path's lengths: exactly the length the walk
@@ -1336,8 +1396,8 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (hipMemsetAsync(tile_long, 0, 4 * L.max_tiles, s) != hipSuccess) return SRPC_E_HIP;
         const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
                               len_at + 8};
-        launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, wire_len,
-               rec_offs, n, lens, spos, st, fast);
+        launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, wire_len,
+               rec_offs, n, lens, spos, st, fast, 0u);
         int rc = launch_scan(SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes},
                              n, partial, str_offs[f], tiles, L.max_tiles, s, kTileBytes, 1, bad);
         if (rc) return rc;
@@ -1348,8 +1408,16 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     }
     if (n) {
         if (!wire) return SRPC_E_INVALID;
-        launch(k_unpack_var_walk, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
-               wire_len, rec_offs, n, lens, spos, st, SingleFast{});
+        // stage a workgroup's span when 1.25x the average span fits 48 KiB
+        const uint64_t avg = wire_len / n;
+        const uint64_t want = avg > kWalkStageMax ? ~0ull : (avg * kBlock * 5 / 4 + 32 + 4095) & ~4095ull;
+        if (want <= kWalkStageMax)
+            launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                   static_cast<uint32_t>(want), s, a, wire, wire_len, rec_offs, n, lens, spos, st, SingleFast{},
+                   static_cast<uint32_t>(want));
+        else
+            launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+                   wire_len, rec_offs, n, lens, spos, st, SingleFast{}, 0u);
     }
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;

@@ -615,3 +615,109 @@ def test_strings_errors(var_kernel):
     got = host(w, int(rec[n])).tobytes()
     assert got[:small] == bytes(oracle.pack(kinds, cols, n, p.prefix, list(offs)))[:small]
     assert set(got[small:]) <= {0xA5}
+
+
+def _model_multi_string(kinds, wire: bytes, n, rec, prefix: bytes):
+    """The general (multi-string) unpack_var semantics on bad input, record
+    by record as k_unpack_var_walk decodes it: BOUNDS (a record outside the
+    wire or shorter than its fixed bytes, a length past the record end, a
+    size that disagrees with the index) decodes every string of the record
+    as empty; fixed fields read before the BOUNDS condition are written; a
+    PREFIX-only record keeps everything.  Returns (status, fixed values
+    {(f, r): bytes}, str_offs per string field, chars per string field)."""
+    fixed = len(prefix) + sum(8 if k == oracle.STRING else oracle.KIND_SIZE[k] for k in kinds)
+    W = len(wire)
+    flags, first = 0, None
+    vals = {}
+    lens = {f: [] for f, k in enumerate(kinds) if k == oracle.STRING}
+    chars = {f: bytearray() for f in lens}
+    for r in range(n):
+        start, end = int(rec[r]), int(rec[r + 1])
+        flag = 0
+        if start > end or end > W or end - start < fixed:
+            flag = srpc_amd.SRPC_STATUS_BOUNDS
+        if not flag and wire[start:start + len(prefix)] != prefix:
+            flag = SRPC_STATUS_PREFIX
+        pos = start + len(prefix)
+        got = {}
+        for f, k in enumerate(kinds):
+            if k != oracle.STRING:
+                sz = oracle.KIND_SIZE[k]
+                if flag != srpc_amd.SRPC_STATUS_BOUNDS:
+                    vals[(f, r)] = bytes(wire[pos:pos + sz])
+                pos += sz
+                continue
+            ln = 0
+            if flag != srpc_amd.SRPC_STATUS_BOUNDS and pos + 8 <= end:
+                ln = int.from_bytes(wire[pos:pos + 8], "little")
+                pos += 8
+                if ln > end - pos:
+                    flag, ln = srpc_amd.SRPC_STATUS_BOUNDS, 0
+            else:
+                flag = srpc_amd.SRPC_STATUS_BOUNDS
+            got[f] = (pos, ln)
+            pos += ln
+        if not flag and pos != end:
+            flag = srpc_amd.SRPC_STATUS_BOUNDS
+        for f in lens:
+            p0, ln = got[f]
+            if flag == srpc_amd.SRPC_STATUS_BOUNDS:
+                ln = 0
+            lens[f].append(ln)
+            chars[f] += wire[p0:p0 + ln]
+        if flag:
+            flags |= flag
+            first = r if first is None else first
+    offs = {f: np.concatenate([[0], np.cumsum(np.array(v, np.uint64))]).astype(np.uint64) for f, v in lens.items()}
+    return (flags, first if first is not None else 2**64 - 1), vals, offs, {f: bytes(c) for f, c in chars.items()}
+
+
+@pytest.mark.parametrize("maxlen", [30, 200])
+def test_multi_strings_errors(maxlen):
+    """Corrupt inputs through the multi-string unpack (the staged walk for
+    short records, the global walk for long ones and for records outside a
+    non-monotonic index) against the model of the general semantics."""
+    kinds = [oracle.INT32, oracle.STRING, oracle.INT16, oracle.STRING, oracle.INT8]
+    n = 3000
+    rng = np.random.default_rng(17)
+    cols, offs = _random_string_batch(kinds, n, rng, maxlen)
+    sch = Schema("M", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker.for_request(sch, "Svc::multi")
+    clean = bytes(oracle.pack(kinds, cols, n, p.prefix, list(offs)))
+    rec = _rec_offsets(kinds, offs, n, len(p.prefix))
+
+    def check(wire, idx):
+        back, boffs, st = gpu_unpack_var(p, kinds, bytes(wire), n, idx)
+        want_st, vals, mo, mc = _model_multi_string(kinds, bytes(wire), n, idx, p.prefix)
+        assert st == want_st
+        for f, k in enumerate(kinds):
+            if k == oracle.STRING:
+                assert np.array_equal(boffs[f], mo[f]), f
+                assert back[f].tobytes() == mc[f], f
+            else:
+                raw = back[f].tobytes()
+                sz = oracle.KIND_SIZE[k]
+                for (g, r), v in vals.items():
+                    if g == f:
+                        assert raw[r * sz:(r + 1) * sz] == v, (f, r)
+
+    check(clean, rec)  # clean input: every record exact
+    wire = bytearray(clean)
+    # the second string's length pointing past its record
+    bad = 1234
+    pos = int(rec[bad]) + len(p.prefix) + 4 + 8 + int(offs[1][bad + 1] - offs[1][bad]) + 2
+    wire[pos:pos + 8] = (10**6).to_bytes(8, "little")
+    # the first string's length one byte short (record size then disagrees)
+    pos2 = int(rec[2000]) + len(p.prefix) + 4
+    ln = int(offs[1][2001] - offs[1][2000])
+    if ln:
+        wire[pos2:pos2 + 8] = (ln - 1).to_bytes(8, "little")
+    # a prefix mismatch in an earlier record
+    wire[int(rec[777]) + 5] ^= 0x01
+    check(wire, rec)
+    # an index that is not monotonic: records 299..300 point backwards
+    rec4 = rec.copy()
+    rec4[300] = rec[310]
+    check(wire, rec4)
+    # a truncated wire: the last records fall outside it
+    check(bytes(wire[:int(rec[n - 5]) + 3]), rec)
