@@ -1003,10 +1003,10 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
 // monotonic) is parsed from global memory with the same code.
 constexpr uint64_t kWalkStageMax = 49152;
 
-// STAGED (multi-string schemas whose average span fits, chosen by the host):
-// the stage is dynamic LDS of stage_bytes.  Single-string schemas walk from
-// global memory: one length per record, and the LDS stage costs them more in
-// occupancy than it saves (0-16 B strings 105 -> 139 us staged).
+// STAGED (chosen by the host when 1.25x the average span fits 48 KiB): the
+// stage is dynamic LDS of exactly stage_bytes -- a fixed 32 KiB stage cost
+// short-record schemas more in occupancy than it saved (0-16 B strings
+// 105 -> 139 us), the sized one gains 4-8 % on them.
 template <bool STAGED>
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
@@ -1396,8 +1396,17 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (hipMemsetAsync(tile_long, 0, 4 * L.max_tiles, s) != hipSuccess) return SRPC_E_HIP;
         const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
                               len_at + 8};
-        launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire, wire_len,
-               rec_offs, n, lens, spos, st, fast, 0u);
+        // the walk stages its span as in the multi-string path when it fits
+        // (0-32 B strings 77 -> 71 us, r01_var_staged_walk_ab.log)
+        const uint64_t avg1 = wire_len / n;
+        const uint64_t want1 = avg1 > kWalkStageMax ? ~0ull : (avg1 * kBlock * 5 / 4 + 32 + 4095) & ~4095ull;
+        if (want1 <= kWalkStageMax)
+            launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                   static_cast<uint32_t>(want1), s, a, wire, wire_len, rec_offs, n, lens, spos, st, fast,
+                   static_cast<uint32_t>(want1));
+        else
+            launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+                   wire_len, rec_offs, n, lens, spos, st, fast, 0u);
         int rc = launch_scan(SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes},
                              n, partial, str_offs[f], tiles, L.max_tiles, s, kTileBytes, 1, bad);
         if (rc) return rc;
