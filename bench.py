@@ -47,6 +47,7 @@ def parse():
                     help="target CPU-baseline work (rank 0, N=1 only); 0 disables")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache kernel clock")
     ap.add_argument("--path", choices=["auto", "dword", "tile"], default="auto")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N>1 on one GPU")
@@ -213,6 +214,26 @@ def main() -> None:
 
     pack_ms = [kev[i][0].elapsed_time(kev[i][1]) for i in range(K)]
     unpack_ms = [kev[i][2].elapsed_time(kev[i][3]) for i in range(K)]
+
+    # Cold-cache kernel clock (SURVEY.md §8d's second regime): 512 MiB written
+    # before every armed call evicts the 256 MiB Infinity Cache (and L2).
+    cold = None
+    if not args.no_cold:
+        flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+        kc = min(K, 10)
+        for i in range(kc):
+            flush.fill_(i & 0xFF)
+            srpc_amd.time_next_call(kev[i][0], kev[i][1])
+            p.pack(cols, n, wire, stream=stream)
+            flush.fill_((i + 1) & 0xFF)
+            srpc_amd.time_next_call(kev[i][2], kev[i][3])
+            p.unpack(wire, n * REC_BYTES, n, back, stream=stream)
+        torch.cuda.synchronize(dev)
+        cp = sorted(kev[i][0].elapsed_time(kev[i][1]) for i in range(kc))[kc // 2]
+        cu = sorted(kev[i][2].elapsed_time(kev[i][3]) for i in range(kc))[kc // 2]
+        cold = {"pack": round(cp, 4), "unpack": round(cu, 4), "reps": kc, "stat": "median",
+                "flush": "512 MiB written before each call (Infinity Cache is 256 MiB)"}
+        del flush
     gpu_ms = step0.elapsed_time(step1)
     t_rank = max(elapsed, gpu_ms / 1e3)
     t = torch.tensor([t_rank, sum(pack_ms) / K, sum(unpack_ms) / K], dtype=torch.float64,
@@ -302,6 +323,7 @@ def main() -> None:
             "hbm_algorithmic_GBps": round(2 * ALG_BYTES_PER_REC * total_recs * K / t_max / 1e9, 1),
             "kernels_ms": {"pack": round(pack_avg, 4), "unpack": round(unpack_avg, 4),
                            "clock": "dispatch begin/end stamped by hipExtLaunchKernel (srpc_time_next_call), K armed steps after the step clock"},
+            "kernels_ms_cold": cold,
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
