@@ -1074,9 +1074,80 @@ struct SingleStrLen {
     }
 };
 
-// Chars of one string field: output chunk c = bytes [16c, 16c+16) of chars.
-// Record r's chars start at spos[r] in the wire, or (single-string schemas,
-// spos == null) at rec_offs[r] + chars_at, staged with the window.
+// Chars of one string field, tile t: output chunk c = bytes [16c, 16c+16) of
+// chars.  Record r's chars start at spos[r] in the wire, or (single-string
+// schemas, spos == null) at rec_offs[r] + chars_at, staged with the window.
+// r0/r1: tile_first[t], tile_first[t + 1].  Block-wide (syncs inside).
+// Head: hoist the chunk's first two segments (multi-string schemas, whose
+// strings are short next to the tile; with 0-1024 B single strings it costs 5 %).
+template <bool Head>
+__device__ __forceinline__ void chars_tile(const uint8_t* __restrict__ wire, uint64_t wire_len,
+                                           const uint64_t* __restrict__ soff, const uint64_t* __restrict__ spos,
+                                           uint64_t n, uint8_t* __restrict__ chars,
+                                           const uint64_t* __restrict__ rec_offs, uint32_t chars_at, uint64_t t,
+                                           uint64_t ntiles, uint64_t total, uint64_t r0, uint64_t r1, uint64_t* win,
+                                           uint64_t* rwin, uint8_t* slots) {
+    const uint64_t lo = t * kTileBytes;
+    const uint64_t rz = t + 1 < ntiles ? max(r1, r0) : n - 1;
+    const Window w = spos ? load_window(soff, n, r0, rz, win) : load_window2(soff, rec_offs, n, r0, rz, win, rwin);
+    const uint64_t p0 = lo + 16ull * threadIdx.x;
+    if (p0 < total) {
+        const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
+        uint64_t r = find_record(soff, n, w, win, p0);
+        uint64_t p = p0;
+        uint32_t b = 0;
+        Slot c{slots + 32 * threadIdx.x};
+        // Head: the chunk's first two segments (records r and r + 1) with
+        // their source offsets and 16-byte wire loads issued together, so
+        // the two (offset -> chars) load chains overlap instead of running
+        // back to back.  The loop below finishes chunks spanning more.
+        if (Head && r < n) {
+            const uint64_t k = r - w.r0;
+            const uint64_t r1 = min(r + 1, n - 1);
+            const uint64_t rs0 = k + 1 < w.len ? win[k] : soff[r];
+            const uint64_t re0 = k + 1 < w.len ? win[k + 1] : soff[r + 1];
+            const uint64_t re1 = k + 2 < w.len ? win[k + 2] : soff[r1 + 1];
+            const uint64_t sp0 = spos ? spos[r] : (k + 1 < w.len ? rwin[k] : rec_offs[r]) + chars_at;
+            const uint64_t sp1 = spos ? spos[r1] : (k + 2 < w.len ? rwin[k + 1] : rec_offs[r1]) + chars_at;
+            const uint32_t cnt0 = static_cast<uint32_t>(min<uint64_t>(nb, re0 - p));
+            const uint64_t p1 = p + cnt0;
+            const uint32_t cnt1 = (cnt0 < nb && r + 1 < n)
+                                      ? static_cast<uint32_t>(min<uint64_t>(nb - cnt0, re1 - p1))
+                                      : 0u;
+            const uint8_t* s0 = wire + sp0 + (p - rs0);
+            const uint8_t* s1 = cnt1 ? wire + sp1 + (p1 - re0) : s0;
+            const uint8_t* end = wire + wire_len;
+            if (s0 + 16 <= end && s1 + 16 <= end) {
+                uint4 v0, v1;
+                __builtin_memcpy(&v0, s0, 16);
+                __builtin_memcpy(&v1, s1, 16);
+                __builtin_memcpy(c.s, &v0, 16);
+                if (cnt1) __builtin_memcpy(c.s + cnt0, &v1, 16);
+            } else {
+                if (cnt0) put(c, s0, 0, static_cast<int>(cnt0), end);
+                if (cnt1) put(c, s1, static_cast<int>(cnt0), static_cast<int>(cnt1), end);
+            }
+            b = cnt0 + cnt1;
+            p = p1 + cnt1;
+            r += cnt0 < nb ? 2 : 1;
+        }
+        while (b < nb && r < n) {
+            const uint64_t k = r - w.r0;
+            const uint64_t rs = k + 1 < w.len ? win[k] : soff[r];
+            const uint64_t re = k + 1 < w.len ? win[k + 1] : soff[r + 1];
+            const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
+            if (cnt) {
+                const uint64_t sp = spos ? spos[r] : (k + 1 < w.len ? rwin[k] : rec_offs[r]) + chars_at;
+                put(c, wire + sp + (p - rs), static_cast<int>(b), static_cast<int>(cnt), wire + wire_len);
+            }
+            b += cnt;
+            p += cnt;
+            ++r;
+        }
+        store_slot(chars + p0, c, nb);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                              const uint64_t* __restrict__ soff,
                                                              const uint64_t* __restrict__ tile_first,
@@ -1098,31 +1169,44 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
         const uint64_t r0 = tile_first[t], r1 = tile_first[min(t + 1, ntiles - 1)];
         asm volatile("" ::"s"(r0), "s"(r1));  // keeps the tile_first loads above the branch
         if (!needed) continue;
-        const uint64_t lo = t * kTileBytes;
-        const uint64_t rz = t + 1 < ntiles ? max(r1, r0) : n - 1;
-        const Window w = spos ? load_window(soff, n, r0, rz, win) : load_window2(soff, rec_offs, n, r0, rz, win, rwin);
-        const uint64_t p0 = lo + 16ull * threadIdx.x;
-        if (p0 < total) {
-            const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, total - p0));
-            uint64_t r = find_record(soff, n, w, win, p0);
-            uint64_t p = p0;
-            uint32_t b = 0;
-            Slot c{slots + 32 * threadIdx.x};
-            while (b < nb && r < n) {
-                const uint64_t k = r - w.r0;
-                const uint64_t rs = k + 1 < w.len ? win[k] : soff[r];
-                const uint64_t re = k + 1 < w.len ? win[k + 1] : soff[r + 1];
-                const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                if (cnt) {
-                    const uint64_t sp = spos ? spos[r] : (k + 1 < w.len ? rwin[k] : rec_offs[r]) + chars_at;
-                    put(c, wire + sp + (p - rs), static_cast<int>(b), static_cast<int>(cnt), wire + wire_len);
-                }
-                b += cnt;
-                p += cnt;
-                ++r;
-            }
-            store_slot(chars + p0, c, nb);
-        }
+        chars_tile<false>(wire, wire_len, soff, spos, n, chars, rec_offs, chars_at, t, ntiles, total, r0, r1, win, rwin,
+                   slots);
+        __syncthreads();
+    }
+}
+
+// Every string field of a multi-string schema in ONE launch, the fields'
+// tiles interleaved (work item u -> field u % nstr, tile u / nstr): tile t of
+// every field covers about the same records, so the wire lines one field's
+// tile pulls in are still in L2 / Infinity Cache when the other fields'
+// tiles read them (separate launches stream the whole wire once per field).
+struct CharsFields {
+    const uint64_t* soff[kMaxFields];
+    const uint64_t* tile_first[kMaxFields];
+    const uint64_t* spos[kMaxFields];
+    uint8_t* chars[kMaxFields];
+    uint32_t nstr;
+};
+
+__global__ __launch_bounds__(kBlock) void k_unpack_var_chars_multi(const uint8_t* __restrict__ wire,
+                                                                   uint64_t wire_len, CharsFields cf, uint64_t n,
+                                                                   uint64_t max_tiles) {
+    __shared__ uint64_t win[kWindow];
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
+    uint64_t nt_max = 0;
+    for (uint32_t j = 0; j < cf.nstr; ++j)
+        nt_max = max(nt_max, min((cf.soff[j][n] + kTileBytes - 1) / kTileBytes, max_tiles));
+    const uint64_t items = nt_max * cf.nstr;
+    for (uint64_t u = blockIdx.x; u < items; u += gridDim.x) {
+        const uint32_t j = static_cast<uint32_t>(u % cf.nstr);
+        const uint64_t t = u / cf.nstr;
+        const uint64_t* soff = cf.soff[j];
+        const uint64_t total = soff[n];
+        const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
+        if (t >= ntiles) continue;
+        const uint64_t r0 = cf.tile_first[j][t], r1 = cf.tile_first[j][min(t + 1, ntiles - 1)];
+        chars_tile<true>(wire, wire_len, soff, cf.spos[j], n, cf.chars[j], nullptr, 0u, t, ntiles, total, r0, r1, win,
+                   nullptr, slots);
         __syncthreads();
     }
 }
@@ -1435,6 +1519,21 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         if (rc) return rc;
     }
     if (n == 0) return SRPC_OK;
+#ifndef SRPC_CHARS_PERFIELD
+    if (p->nstrings > 1) {  // one interleaved launch: the wire is streamed once, not once per field
+        CharsFields cf{};
+        for (uint32_t f = 0; f < p->nfields; ++f) {
+            if (p->size[f]) continue;
+            const uint32_t j = cf.nstr++;
+            cf.soff[j] = str_offs[f];
+            cf.tile_first[j] = tiles + a.sidx[f] * L.max_tiles;
+            cf.spos[j] = spos + a.sidx[f] * n;
+            cf.chars[j] = static_cast<uint8_t*>(cols[f]);
+        }
+        launch(k_unpack_var_chars_multi, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, cf, n, L.max_tiles);
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
+#endif
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f],

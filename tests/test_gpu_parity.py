@@ -505,6 +505,44 @@ def test_strings_random_vs_oracle(n, schema, maxlen, envelope, var_kernel):
             assert np.array_equal(boffs[f], ooffs[f])
 
 
+@pytest.mark.parametrize("maxlens", [(0, 700), (3, 0, 900), (700, 2, 40), (0, 0)])
+@pytest.mark.parametrize("n", [1, 257, 6000])
+def test_strings_skewed_fields_vs_oracle(n, maxlens):
+    """Multi-string unpack copies every field's chars in one launch, the
+    fields' 4 KiB tiles interleaved: fields whose chars span very different
+    tile counts (all empty, a few bytes, hundreds of bytes per record)."""
+    kinds = []
+    for i in range(len(maxlens)):
+        kinds += [oracle.STRING, oracle.INT16 if i % 2 else oracle.INT64]
+    rng = np.random.default_rng(n * 7 + len(maxlens))
+    cols, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            m = maxlens[len([o for o in offs if o is not None])]
+            lens = rng.integers(0, m + 1, n).astype(np.uint64)
+            o = np.zeros(n + 1, np.uint64)
+            o[1:] = np.cumsum(lens)
+            cols.append(rng.integers(0, 256, max(1, int(o[-1])), dtype=np.uint8))
+            offs.append(o)
+        else:
+            dt = np.dtype(oracle.KIND_DTYPE[k])
+            cols.append(rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt))
+            offs.append(None)
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker.for_request(sch, "Svc_servicer::skew")
+    want = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st[0] == 0 and wire == want
+    back, boffs, st = gpu_unpack_var(p, kinds, want, n, rec)
+    assert st[0] == 0
+    rc, ocols, ooffs, _, _ = oracle.unpack(kinds, want, n, p.prefix)
+    assert rc == 0
+    for f, k in enumerate(kinds):
+        assert back[f].tobytes() == ocols[f].tobytes(), f
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f], ooffs[f])
+
+
 @pytest.mark.parametrize("chars_shift,offs_shift", [(0, 0), (3, 8), (15, 8), (1, 0)])
 def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift, var_kernel):
     """Chars columns and offset arrays at any byte / 8-byte alignment, strings
