@@ -350,12 +350,14 @@ __device__ unsigned long long g_phase[8];
 // bytes [b, b + cnt).  Segments in wire order: prefix, then every field
 // (fixed value | u64 length, chars).  sw (may be null): LDS copy of
 // soff[f0][r], soff[f0][r+1] for the first string field f0.
-__device__ __forceinline__ void emit_record(const VarArgs& a, const uint64_t* climit, uint32_t f0, const uint64_t* sw,
-                                            uint64_t n, uint64_t r, uint64_t q, uint32_t cnt, int b, Slot& c) {
+// pre: the prefix followed by 16 zero bytes (LDS copy in k_pack_var).
+__device__ __forceinline__ void emit_record(const VarArgs& a, const uint8_t* pre, const uint64_t* climit, uint32_t f0,
+                                            const uint64_t* sw, uint64_t n, uint64_t r, uint64_t q, uint32_t cnt,
+                                            int b, Slot& c) {
     const uint64_t end = q + cnt;
     if (q < a.prefix_len) {
         const int k = static_cast<int>(min<uint64_t>(end, a.prefix_len) - q);
-        put(c, a.prefix + q, b, k, a.prefix + a.prefix_len + 16);
+        put(c, pre + q, b, k, pre + a.prefix_len + 16);
         b += k;
         q += k;
     }
@@ -405,6 +407,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
     __shared__ uint64_t swin[kWindow];       // char offsets of the first string field, same records
     __shared__ uint64_t climit[kMaxFields];  // end of each string field's chars
     __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
+#ifndef SRPC_PACK_PREFIX_GLOBAL
+    // the prefix segment is read from LDS: no L2 round trip per chunk that starts a record
+    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
+    if (a.prefix_len)  // no device prefix (null) when the plan has none
+        for (uint32_t i = threadIdx.x; i < a.prefix_len + 16; i += kBlock) pre[i] = a.prefix[i];
+#else
+    const uint8_t* pre = a.prefix;
+#endif
     uint32_t f0 = 0;                         // the first string field
     while (a.size[f0]) ++f0;
     for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
                 const uint64_t rs = k + 1 < w.len ? win[k] : rec_offs[r];
                 const uint64_t re = k + 1 < w.len ? win[k + 1] : rec_offs[r + 1];
                 const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(nb - b, re - p));
-                emit_record(a, climit, f0, k + 1 < w.len ? swin + k : nullptr, n, r, p - rs, cnt,
+                emit_record(a, pre, climit, f0, k + 1 < w.len ? swin + k : nullptr, n, r, p - rs, cnt,
                             static_cast<int>(b), c);
                 b += cnt;
                 p += cnt;
