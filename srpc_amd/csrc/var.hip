@@ -79,6 +79,19 @@ struct ArrayVals {
     __device__ uint64_t operator()(uint64_t i) const { return v[i]; }
 };
 
+// Batched scan of every string field's lengths in one launch per phase:
+// domain y = blockIdx.y = string ordinal, values v[y * n + i], output outs[y].
+// The scan kernels offset partial and tile_first by y (a no-op for y = 0).
+struct ArrayValsY {
+    const uint64_t* v;
+    uint64_t n;
+    uint64_t* outs[kMaxFields];
+    __device__ uint64_t operator()(uint64_t i) const { return v[blockIdx.y * n + i]; }
+};
+template <class F>
+__device__ __forceinline__ uint64_t* scan_out(const F&, uint64_t* out) { return out; }
+__device__ __forceinline__ uint64_t* scan_out(const ArrayValsY& f, uint64_t* /*out*/) { return f.outs[blockIdx.y]; }
+
 // Tile metadata written by the scan for every tile whose first byte item i
 // covers: item i itself (stride 1), which is all the chunk-walk kernels need.
 struct FirstOnly {
@@ -155,12 +168,13 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_
     }
     uint64_t tot;
     (void)block_exclusive_scan(s, &tot);
-    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+    if (threadIdx.x == 0) partial[blockIdx.y * (gridDim.x + 1ull) + blockIdx.x] = tot;
 }
 
 // One workgroup: exclusive scan of nb partials in place, partial[nb] = total.
 __global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uint64_t nb, const uint32_t* gate) {
     if (gate && *gate == 0) return;
+    partial += blockIdx.y * (nb + 1);
     const uint64_t per = (nb + kBlock - 1) / kBlock;
     const uint64_t lo = threadIdx.x * per, hi = min(nb, lo + per);
     uint64_t s = 0;
@@ -186,6 +200,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
                                                        uint64_t tile_bytes, uint32_t meta_stride,
                                                        const uint32_t* gate) {
     if (gate && *gate == 0) return;
+    partial += blockIdx.y * (nb + 1);
+    out = scan_out(f, out);
+    if (tile_first) tile_first += blockIdx.y * max_tiles * meta_stride;
     __shared__ uint64_t v[kScanBlock];
     const uint64_t base = blockIdx.x * kScanBlock;
 #pragma unroll
@@ -1275,12 +1292,12 @@ StagedLayout staged_layout(const srpc_plan* p, uint32_t T) {
 template <class F, class M = FirstOnly>
 int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* tile_first, uint64_t max_tiles,
                 hipStream_t s, uint64_t tile_bytes = kTileBytes, uint32_t meta_stride = 1,
-                const uint32_t* gate = nullptr) {
+                const uint32_t* gate = nullptr, uint32_t domains = 1) {
     const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
     if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, n, partial, gate);
-    launch(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partial, nb, gate);
-    launch(k_scan_apply<F, M>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, f, M{}, n, partial, nb, out,
+    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb), domains), dim3(kBlock), 0, s, f, n, partial, gate);
+    launch(k_scan_partials, dim3(1, domains), dim3(kBlock), 0, s, partial, nb, gate);
+    launch(k_scan_apply<F, M>, dim3(static_cast<uint32_t>(nb), domains), dim3(kBlock), 0, s, f, M{}, n, partial, nb, out,
            tile_first, max_tiles, tile_bytes, meta_stride, gate);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
@@ -1326,8 +1343,9 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     ScratchLayout L{};
     L.max_tiles = wire_bytes / kTileBytes + 2;
     L.partial_off = 0;
-    L.tiles_off = round256(8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1));
     const uint64_t domains = unpack ? p->nstrings : 1 + p->nstrings;
+    // one partials array per string field: multi-string unpack scans them all in one launch
+    L.tiles_off = round256(8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1) * std::max<uint64_t>(1, domains));
     L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
     L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
     L.bad_off = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
@@ -1522,6 +1540,15 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
             launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
                    wire_len, rec_offs, n, lens, spos, st, SingleFast{}, 0u);
     }
+#ifndef SRPC_SCAN_PERFIELD
+    if (p->nstrings > 1) {  // all string fields' offsets in one scan launch per phase
+        ArrayValsY fy{lens, n, {}};
+        for (uint32_t f = 0; f < p->nfields; ++f)
+            if (!p->size[f]) fy.outs[a.sidx[f]] = str_offs[f];
+        int rc = launch_scan(fy, n, partial, nullptr, tiles, L.max_tiles, s, kTileBytes, 1, nullptr, p->nstrings);
+        if (rc) return rc;
+    } else
+#endif
     for (uint32_t f = 0; f < p->nfields; ++f) {
         if (p->size[f]) continue;
         int rc = launch_scan(ArrayVals{lens + a.sidx[f] * n}, n, partial, str_offs[f],
