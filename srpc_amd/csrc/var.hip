@@ -1238,7 +1238,6 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars_multi(const uint8_t
     }
 }
 
-__global__ void k_set_flag(uint32_t* f) { *f = 1; }
 
 // bad: nflags u32 flags, 64 bytes apart.
 __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t nflags) {
@@ -1438,22 +1437,28 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     if (n && !wire) return SRPC_E_INVALID;
     uint32_t* some_long = reinterpret_cast<uint32_t*>(base + L.bad_off);
-    hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
     // records that may be written one per lane: small ones only (wide per-lane
     // records write partial cache lines: 94-byte records took 723 us against
     // the walk's 313, profiles/r01_var_pack_short_ab.log)
     const bool small = p->fixed_bytes + p->nstrings * kShortCopy <= kShortRecord;
+    // skip_test: k_pack_short_records ran and its flags say whether the walk
+    // has work; otherwise the walk runs unconditionally (k_pack_var<false>,
+    // no flag reset / set launches: 2 tiny kernels, ~7 us)
+    bool skip_test = true;
     if (p->nstrings == 1) {
+        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
         launch(k_pack_short_records<true>, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs,
                tiles, some_long, L.max_tiles, wire, small ? wire_cap : 0);
     } else {
         int rc = launch_scan(PackSizes{a}, n, partial, rec_offs, tiles, L.max_tiles, s);
         if (rc) return rc;
-        if (n && small)
+        if (n && small) {
+            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, some_long, kLongFlags);
             launch(k_pack_short_records<false>, dim3(static_cast<uint32_t>(g1)), dim3(kBlock), 0, s, a, n, rec_offs,
                    tiles, some_long, L.max_tiles, wire, wire_cap);
-        else
-            hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, s, some_long);
+        } else {
+            skip_test = false;
+        }
     }
     if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (!wire) return SRPC_E_INVALID;
@@ -1463,8 +1468,8 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     // profiles/r01_var_short_copy_ab.log)
     uint32_t f0 = 0;
     while (p->size[f0]) ++f0;
-    launch(k_pack_var<true>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n, tiles, wire, wire_cap, st,
-           static_cast<const uint32_t*>(some_long), a.soff[f0]);
+    launch(skip_test ? k_pack_var<true> : k_pack_var<false>, dim3(kVarGrid), dim3(kBlock), 0, s, a, rec_offs, n,
+           tiles, wire, wire_cap, st, static_cast<const uint32_t*>(some_long), a.soff[f0]);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
