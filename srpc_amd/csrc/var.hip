@@ -1029,8 +1029,21 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
 // record outside the staged span (a long span, or an index that is not
 // monotonic) is parsed from global memory with the same code.
 constexpr uint64_t kWalkStageMax = 49152;
+#ifndef SRPC_STAGE_NUM
+#define SRPC_STAGE_NUM 17
+#define SRPC_STAGE_DEN 16
+#define SRPC_STAGE_ROUND 512
+#endif
+// LDS stage of the unpack walk for an average record of avg bytes: the
+// workgroup's 256 records with 6 % slack (a wider span parses from global;
+// correct either way).  5/4 rounded to 4 KiB staged 32 KiB for ~100-byte
+// records (4 workgroups per CU); 17/16 rounded to 512 B stages 27.5 KiB (5):
+// two strings + envelope unpack 380 -> 361 us (r01_var_stage_slack_ab.log).
+inline uint64_t stage_bytes_for(uint64_t avg) {
+    return (avg * kBlock * SRPC_STAGE_NUM / SRPC_STAGE_DEN + 32 + SRPC_STAGE_ROUND - 1) & ~(SRPC_STAGE_ROUND - 1ull);
+}
 
-// STAGED (chosen by the host when 1.25x the average span fits 48 KiB): the
+// STAGED (chosen by the host when 17/16 of the average span fits 48 KiB): the
 // stage is dynamic LDS of exactly stage_bytes -- a fixed 32 KiB stage cost
 // short-record schemas more in occupancy than it saved (0-16 B strings
 // 105 -> 139 us), the sized one gains 4-8 % on them.
@@ -1516,7 +1529,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         // the walk stages its span as in the multi-string path when it fits
         // (0-32 B strings 77 -> 71 us, r01_var_staged_walk_ab.log)
         const uint64_t avg1 = wire_len / n;
-        const uint64_t want1 = avg1 > kWalkStageMax ? ~0ull : (avg1 * kBlock * 5 / 4 + 32 + 4095) & ~4095ull;
+        const uint64_t want1 = avg1 > kWalkStageMax ? ~0ull : stage_bytes_for(avg1);
         if (want1 <= kWalkStageMax)
             launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
                    static_cast<uint32_t>(want1), s, a, wire, wire_len, rec_offs, n, lens, spos, st, fast,
@@ -1534,9 +1547,9 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     }
     if (n) {
         if (!wire) return SRPC_E_INVALID;
-        // stage a workgroup's span when 1.25x the average span fits 48 KiB
+        // stage a workgroup's span when 17/16 of the average span fits 48 KiB
         const uint64_t avg = wire_len / n;
-        const uint64_t want = avg > kWalkStageMax ? ~0ull : (avg * kBlock * 5 / 4 + 32 + 4095) & ~4095ull;
+        const uint64_t want = avg > kWalkStageMax ? ~0ull : stage_bytes_for(avg);
         if (want <= kWalkStageMax)
             launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
                    static_cast<uint32_t>(want), s, a, wire, wire_len, rec_offs, n, lens, spos, st, SingleFast{},
