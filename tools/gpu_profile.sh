@@ -6,7 +6,7 @@ R=${1:-r01}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 BENCH="python3 bench.py --cpu-seconds 0 --no-pcie --no-verify"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_${R}.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- $BENCH --steps 20 --warmup 3 > gpurun_out/prof_stats.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o run --output-format csv -- $BENCH --steps 5 --warmup 1 > gpurun_out/prof_fetch.log 2>&1 || exit 4
