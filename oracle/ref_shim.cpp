@@ -28,6 +28,9 @@
 // by the reference tool from examples/calculator.contract.
 #include "calculator_srpc.cpp"
 
+// deterministic Geo records shared with tests/cpp/batchgen_gpu_test.cpp
+#include "../tests/cpp/geo_records.hpp"
+
 namespace {
 
 // Synthetic schema of configs 3/4: message Quad { int32 a,b,c,d; }
@@ -128,6 +131,46 @@ struct all_kinds : public srpc::message_base {
         p >> k_i64;
     }
 };
+
+// The messages of tests/cpp/batchgen_example.contract (the f3 pin), written
+// the way the reference generator emits a message (generator.hpp:100-134:
+// fields in declaration order, one STRUCT_MEMBER each, nested messages as
+// members).  Only packing is used: the generator's nested unpack does not
+// compile (generator.hpp:127), so these structs have no nested unpack.
+namespace geo_ref {
+struct Inner : public srpc::message_base {
+    int8_t tag;
+    int16_t small;
+    static constexpr const char* name = "Inner";
+    static constexpr auto fields =
+        std::make_tuple(STRUCT_MEMBER(Inner, tag, "Inner::tag"), STRUCT_MEMBER(Inner, small, "Inner::small"));
+    void unpack(srpc::buffer::ptr) override {}
+};
+struct Point : public srpc::message_base {
+    int32_t x;
+    int32_t y;
+    static constexpr const char* name = "Point";
+    static constexpr auto fields =
+        std::make_tuple(STRUCT_MEMBER(Point, x, "Point::x"), STRUCT_MEMBER(Point, y, "Point::y"));
+    void unpack(srpc::buffer::ptr) override {}
+};
+struct Record : public srpc::message_base {
+    int64_t id;
+    Inner in;
+    bool flag;
+    std::string label;
+    char c;
+    Point p;
+    std::string note;
+    static constexpr const char* name = "Record";
+    static constexpr auto fields = std::make_tuple(
+        STRUCT_MEMBER(Record, id, "Record::id"), STRUCT_MEMBER(Record, in, "Record::in"),
+        STRUCT_MEMBER(Record, flag, "Record::flag"), STRUCT_MEMBER(Record, label, "Record::label"),
+        STRUCT_MEMBER(Record, c, "Record::c"), STRUCT_MEMBER(Record, p, "Record::p"),
+        STRUCT_MEMBER(Record, note, "Record::note"));
+    void unpack(srpc::buffer::ptr) override {}
+};
+}  // namespace geo_ref
 
 struct Calc : public Calculator_servicer {
     Number square(Number& req) override {
@@ -484,6 +527,38 @@ int ref_unpack_square_responses(const uint8_t* resp, uint64_t resp_size, uint64_
         code_out[i] = m.code();
     }
     return 0;
+}
+
+// ---- generated-message batches --------------------------------
+// n Geo.locate responses (pack_response<Record>, code RPC_SUCCESS) and n
+// Geo.locate requests (pack_request<Point>, method "Geo_servicer::locate", the
+// name generator.hpp:84 gives it), records drawn by geo_fixture from `seed`,
+// each stream concatenated in one packer as a server / client appends them.
+uint64_t ref_geo_locate_responses(uint64_t n, uint64_t seed, uint8_t* out, uint64_t cap) {
+    srpc::packer p;
+    uint64_t s = seed;
+    for (uint64_t i = 0; i < n; ++i) {
+        geo_ref::Record r;
+        geo_fixture::fill_record(r, s);
+        srpc::response_t<geo_ref::Record> resp;
+        resp.set_value(r);
+        p.pack_response(resp);
+    }
+    return copy_out(p, out, cap);
+}
+
+uint64_t ref_geo_locate_requests(uint64_t n, uint64_t seed, uint8_t* out, uint64_t cap) {
+    srpc::packer p;
+    uint64_t s = seed;
+    for (uint64_t i = 0; i < n; ++i) {
+        geo_ref::Point pt;
+        geo_fixture::fill_point(pt, s);
+        srpc::request_t<geo_ref::Point> req;
+        req.set_method_name("Geo_servicer::locate");
+        req.set_value(std::move(pt));
+        p.pack_request(req);
+    }
+    return copy_out(p, out, cap);
 }
 
 }  // extern "C"

@@ -960,6 +960,9 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
     for (uint32_t f = 0; f < a.nfields; ++f) {
         const uint32_t sz = a.size[f];
         if (sz) {
+            // a fixed field past the record end is never read (it could lie
+            // past the wire buffer): the record is BOUNDS from here on
+            if (flag != SRPC_STATUS_BOUNDS && pos + sz > end) flag = SRPC_STATUS_BOUNDS;
             if (flag != SRPC_STATUS_BOUNDS) {
                 uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
                 const uint8_t* q = src + (pos - start);
@@ -997,9 +1000,16 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
         const uint64_t o = start - first - r * a.fixed_bytes;  // the output offset if every record is exact
         fast.soff1[r] = o;
         if (r == n - 1) fast.soff1[n] = fast.last - first - n * a.fixed_bytes;
-        // exact: the decoded length (0 for BOUNDS) is the index's size - fixed_bytes
-        const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end;
         const uint64_t len = end - start - a.fixed_bytes;
+        // exact: the decoded length (0 for BOUNDS) is the index's size - fixed_bytes,
+        // and o is a real output offset.  o is only right when every earlier
+        // record is exact too; when one is not (an empty frame, a non-monotonic
+        // index), o can wrap or exceed the chars buffer (wire_len bytes), so a
+        // record whose o + len does not fit is not exact either: *bad then
+        // reruns the offsets through the scan and the chars kernel copies
+        // every tile.  This keeps the walk's own copy inside the buffer.
+        const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end && start >= first &&
+                           start - first >= r * a.fixed_bytes && o <= wire_len && len <= wire_len - o;
         // a wave whose strings are all short copies them here; otherwise its
         // strings' chars tiles are left to k_unpack_var_chars
         const bool all_short = __all(exact && len <= kShortCopy);
@@ -1031,9 +1041,17 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
 constexpr uint64_t kWalkStageMax = 49152;
 #ifndef SRPC_STAGE_NUM
 #define SRPC_STAGE_NUM 17
+#endif
+#ifndef SRPC_STAGE_DEN
 #define SRPC_STAGE_DEN 16
+#endif
+#ifndef SRPC_STAGE_ROUND
 #define SRPC_STAGE_ROUND 512
 #endif
+// the stage copy writes whole 16-byte chunks up to stage_bytes
+static_assert((SRPC_STAGE_ROUND & (SRPC_STAGE_ROUND - 1)) == 0, "SRPC_STAGE_ROUND must be a power of two");
+static_assert(SRPC_STAGE_ROUND % 16 == 0, "SRPC_STAGE_ROUND must be a multiple of 16");
+static_assert(SRPC_STAGE_NUM >= SRPC_STAGE_DEN, "the stage must hold at least the average span");
 // LDS stage of the unpack walk for an average record of avg bytes: the
 // workgroup's 256 records with 6 % slack (a wider span parses from global;
 // correct either way).  5/4 rounded to 4 KiB staged 32 KiB for ~100-byte

@@ -1,16 +1,22 @@
 // needs: gpu, batchgen
-// Generated batch views (srpc_amd.batchgen) driving the GPU batch path: a
-// Record_batch (nested + strings) packed as Geo.locate responses and a
-// Point_batch packed as Geo.locate requests must equal the scalar packer's
-// pack_response / pack_request loops, and unpack must give the columns back.
+// Generated batch views (srpc_amd.batchgen) driving the GPU batch
+// path, pinned to the REFERENCE packer: the Geo.locate records of
+// tests/cpp/geo_records.hpp are packed on the GPU as Record responses (nested
+// + two strings, VAR path) and as Point requests (TILE path), and the bytes are
+// written to <out_dir>/geo_locate_{responses,requests}.bin.
+// tests/test_batchgen.py hashes them against the digests the reference
+// produced from the same records (tests/golden/manifest.json "batchgen",
+// oracle/ref_shim.cpp ref_geo_locate_*).  Unpack must give the columns back.
 #include <hip/hip_runtime_api.h>
 #include <batchgen_example_batch.hpp>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
-#include <random>
+#include <string>
 #include <vector>
+
+#include "geo_records.hpp"
 
 static int g_fail = 0, g_pass = 0;
 #define CHECK(c)                                                                                  \
@@ -47,30 +53,28 @@ static void release(B& b) {
     }
 }
 
-int main() {
-    std::mt19937_64 rng(7);
-    const size_t n = 20000;
+static bool write_file(const std::string& path, const std::vector<uint8_t>& b) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = std::fwrite(b.data(), 1, b.size(), f) == b.size();
+    return std::fclose(f) == 0 && ok;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <out_dir>\n", argv[0]);
+        return 2;
+    }
+    const std::string out_dir = argv[1];
+    const size_t n = geo_fixture::kRecords;
+    uint64_t seed = geo_fixture::kSeed;
     // ---- Geo.locate responses: Record (nested + two strings), variable-size path
     std::vector<Record> recs(n);
+    uint64_t chars = 0;
     for (auto& r : recs) {
-        r.id = static_cast<int64_t>(rng());
-        r.in.tag = static_cast<int8_t>(rng());
-        r.in.small = static_cast<int16_t>(rng());
-        r.flag = rng() & 1;
-        r.label.assign(rng() % 40, 'a');
-        for (auto& ch : r.label) ch = static_cast<char>('a' + rng() % 26);
-        r.c = static_cast<char>(rng());
-        r.p.x = static_cast<int32_t>(rng());
-        r.p.y = static_cast<int32_t>(rng());
-        r.note.assign(rng() % 5 == 0 ? rng() % 300 : 0, 'n');
+        geo_fixture::fill_record(r, seed);
+        chars += r.label.size() + r.note.size();
     }
-    srpc::packer ref;
-    for (auto& r : recs) {
-        srpc::response_t<Record> resp;
-        resp.set_value(Record(r));
-        ref.pack_response(resp);
-    }
-    const std::vector<uint8_t> want(*ref.buf());
     srpc::gpu::host_columns<Record> hc;
     hc.scatter(recs);
     Record_batch rb;
@@ -80,14 +84,19 @@ int main() {
     uint8_t* dw = nullptr;
     uint64_t* drec = nullptr;
     void* scratch = nullptr;
-    const uint64_t sb = resp.scratch_bytes(n, want.size());
-    HIPCHECK(hipMalloc(&dw, want.size() + 16));
+    const uint64_t cap = n * 128 + chars;  // > prefix + fixed fields + lengths per record, plus the chars
+    const uint64_t sb = resp.scratch_bytes(n, cap);
+    HIPCHECK(hipMalloc(&dw, cap + 16));
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&drec), 8 * (n + 1)));
     HIPCHECK(hipMalloc(&scratch, sb + 16));
-    CHECK(resp.pack_var(rb.columns(), rb.str_offsets(), n, dw, want.size(), drec, scratch, sb) == SRPC_OK);
-    std::vector<uint8_t> got(want.size());
+    CHECK(resp.pack_var(rb.columns(), rb.str_offsets(), n, dw, cap, drec, scratch, sb) == SRPC_OK);
+    uint64_t total = 0;
+    HIPCHECK(hipMemcpy(&total, drec + n, 8, hipMemcpyDeviceToHost));
+    CHECK(total > 0 && total <= cap);
+    std::vector<uint8_t> got(std::min(total, cap));
     HIPCHECK(hipMemcpy(got.data(), dw, got.size(), hipMemcpyDeviceToHost));
-    CHECK(got == want);
+    CHECK(write_file(out_dir + "/geo_locate_responses.bin", got));
+    const std::vector<uint8_t>& want = got;
     // unpack into a second batch view and compare the columns
     Record_batch back;
     back.n = n;
@@ -116,29 +125,19 @@ int main() {
 
     // ---- Geo.locate requests: Point, fixed-size path
     std::vector<Point> pts(n);
-    for (auto& p : pts) {
-        p.x = static_cast<int32_t>(rng());
-        p.y = static_cast<int32_t>(rng());
-    }
-    srpc::packer pref;
-    for (auto& p : pts) {
-        srpc::request_t<Point> q;
-        q.set_method_name(Geo_batch::locate_method);
-        q.set_value(Point(p));
-        pref.pack_request(q);
-    }
-    const std::vector<uint8_t> pwant(*pref.buf());
+    seed = geo_fixture::kSeed;  // the reference draws the request stream from the seed again
+    for (auto& p : pts) geo_fixture::fill_point(p, seed);
     srpc::gpu::host_columns<Point> phc;
     phc.scatter(pts);
     Point_batch pb;
     if (upload(phc, pb)) return 2;
     auto req = Geo_batch::locate_request();
-    CHECK(req.record_bytes() * n == pwant.size());
-    HIPCHECK(hipMalloc(&dw, pwant.size() + 16));
-    CHECK(req.pack(pb.columns(), n, dw, pwant.size()) == SRPC_OK);
-    std::vector<uint8_t> pgot(pwant.size());
+    const uint64_t pbytes = req.record_bytes() * n;
+    HIPCHECK(hipMalloc(&dw, pbytes + 16));
+    CHECK(req.pack(pb.columns(), n, dw, pbytes) == SRPC_OK);
+    std::vector<uint8_t> pgot(pbytes);
     HIPCHECK(hipMemcpy(pgot.data(), dw, pgot.size(), hipMemcpyDeviceToHost));
-    CHECK(pgot == pwant);
+    CHECK(write_file(out_dir + "/geo_locate_requests.bin", pgot));
     release(pb);
     (void)hipFree(dw);
 

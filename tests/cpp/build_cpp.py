@@ -57,7 +57,8 @@ def build_one(src: str) -> str:
     os.makedirs(OUT, exist_ok=True)
     exe = exe_path(src)
     req = needs(src)
-    deps = [src] + glob.glob(os.path.join(ROOT, "include", "**", "*"), recursive=True)
+    deps = [src] + glob.glob(os.path.join(ROOT, "include", "**", "*"), recursive=True) + \
+        glob.glob(os.path.join(HERE, "*.hpp"))
     if "batchgen" in req:
         deps.append(generate_batch_header())
     if os.path.exists(exe) and os.path.getmtime(exe) > max(os.path.getmtime(p) for p in deps if os.path.isfile(p)):

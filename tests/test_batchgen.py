@@ -1,6 +1,7 @@
 """srpc_amd.batchgen: contract parsing, the emitted batch
 views and message structs (golden header), their use by the scalar packer
 (host C++), and -- on a GPU -- by the batch path."""
+import hashlib
 import os
 import subprocess
 
@@ -84,12 +85,21 @@ def test_companions_compile_with_reference_generated_stubs(tmp_path):
 
 
 @pytest.mark.gpu
-def test_generated_batch_views_on_gpu():
+def test_generated_batch_views_on_gpu(tmp_path, manifest):
+    """The generated Record_batch / Point_batch views packed on the GPU give
+    exactly the bytes the REFERENCE packer produced for the same records
+    (tests/cpp/geo_records.hpp; digests from oracle/ref_shim.cpp via
+    tests/golden/make_golden.py), and unpack gives the columns back."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from srpc_amd import build
-    build.build()
-    exe = build_cpp.build_one(os.path.join(HERE, "cpp", "batchgen_gpu_test.cpp"))
-    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    exe = build_cpp.exe_path(os.path.join(HERE, "cpp", "batchgen_gpu_test.cpp"))
+    if not os.path.exists(exe):  # built in the build container (build_cpp.build_all)
+        exe = build_cpp.build_one(os.path.join(HERE, "cpp", "batchgen_gpu_test.cpp"))
+    out = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "0 failed" in out.stdout, out.stdout + out.stderr
+    ref = manifest["batchgen"]
+    for label in ("geo_locate_responses", "geo_locate_requests"):
+        got = (tmp_path / f"{label}.bin").read_bytes()
+        assert len(got) == ref[label]["bytes"], label
+        assert hashlib.sha256(got).hexdigest() == ref[label]["sha256"], label

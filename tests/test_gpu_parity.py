@@ -655,6 +655,28 @@ def test_strings_errors(var_kernel):
     assert set(got[small:]) <= {0xA5}
 
 
+def test_strings_empty_frames_then_short_records():
+    """A block of zero-size records (empty frames: rec[i] == rec[i + 1]) in
+    front of short valid records.  Every later record's fast-path output
+    offset start - rec[0] - r * fixed_bytes would wrap below zero; the walk
+    must treat those records as not exact (no copy of its own) and the
+    general path must decode them as the model says."""
+    kinds = [oracle.INT32, oracle.STRING]
+    m, k = 2000, 700
+    rng = np.random.default_rng(23)
+    cols, offs = _random_string_batch(kinds, m, rng, 4)
+    p = GpuPacker.for_request(Schema("E", (("x", oracle.INT32), ("s", oracle.STRING))), "Svc::m")
+    wire = bytes(oracle.pack(kinds, cols, m, p.prefix, list(offs)))
+    rec = _rec_offsets(kinds, offs, m, len(p.prefix))
+    for lead in (np.zeros(k, np.uint64), np.full(k, rec[m], np.uint64)):
+        idx = np.concatenate([lead, rec]) if lead[0] == 0 else np.concatenate([rec, lead])
+        n = m + k
+        back, boffs, st = gpu_unpack_var(p, kinds, wire, n, idx)
+        assert st[0] == srpc_amd.SRPC_STATUS_BOUNDS
+        assert st[1] == (0 if lead[0] == 0 else m)
+        _check_single_string(kinds, back, boffs, wire, n, idx, p.prefix)
+
+
 def _model_multi_string(kinds, wire: bytes, n, rec, prefix: bytes):
     """The general (multi-string) unpack_var semantics on bad input, record
     by record as k_unpack_var_walk decodes it: BOUNDS (a record outside the
@@ -681,6 +703,8 @@ def _model_multi_string(kinds, wire: bytes, n, rec, prefix: bytes):
         for f, k in enumerate(kinds):
             if k != oracle.STRING:
                 sz = oracle.KIND_SIZE[k]
+                if flag != srpc_amd.SRPC_STATUS_BOUNDS and pos + sz > end:
+                    flag = srpc_amd.SRPC_STATUS_BOUNDS  # never read past the record end
                 if flag != srpc_amd.SRPC_STATUS_BOUNDS:
                     vals[(f, r)] = bytes(wire[pos:pos + sz])
                 pos += sz
