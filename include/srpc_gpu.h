@@ -125,14 +125,6 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
                                         (1024..49152), pack and unpack           */
 #define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
-#define SRPC_TUNE_TILE_KERNEL 6      /* TILE path kernel: 0 = LDS image (stride-S
-                                        scatter/gather), 1 = register-assembled
-                                        16-byte chunks from aligned column slabs */
-#define SRPC_TUNE_VAR_KERNEL 7       /* VAR pack kernel: 0 = chunk walk with global
-                                        segment loads (default), 1 = LDS-staged
-                                        tiles (LDS-DMA sources, slower on MI355X) */
-#define SRPC_TUNE_VAR_TILE 8         /* VAR staged pack: output bytes per tile
-                                        (4096..32768, multiple of 4096)          */
 #define SRPC_TUNE_GRID 5             /* DWORD path: max workgroups (0 = one per
                                         256*iter records; else grid-stride)       */
 int srpc_plan_tune(srpc_plan* plan, int knob, int value);

@@ -1,7 +1,6 @@
 // plan.h -- internal: the srpc_plan object and helpers shared by the kernel
 // translation units of libsrpc_gpu.so (srpc_gpu.hip: fixed-size records,
-// chunk.hip: the TILE path's register-assembled kernels, var.hip: records
-// with string fields).  Not part of the public ABI.
+// var.hip: records with string fields).  Not part of the public ABI.
 #pragma once
 
 #include <hip/hip_ext.h>
@@ -114,28 +113,6 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
     }
 }
 
-// TILE path, CHUNK kernel (chunk.hip): kernel arguments and the plan's table.
-struct ChunkArgs {
-    const uint8_t* col[kMaxFields];  // field columns (pack: sources, unpack: destinations)
-    uint32_t lg[kMaxFields];         // log2(field size)
-    uint32_t slab_off[kMaxFields];   // LDS slab of each field: R * (bytes of the fields before)
-    const uint8_t* table;            // device blob: tmpl[P][16] | pmask[P][16] | ent[P][emax]
-    uint32_t table_bytes;            // multiple of 16
-    uint32_t slab_bytes;             // R * field bytes (multiple of 16)
-    uint32_t nfields, stride, prefix_len, R, P, rpp, emax;
-};
-
-// An occurrence of a field in a chunk phase: record q of the period, log2
-// size, first byte at chunk position pos (-7..15), the field's LDS slab.
-inline uint32_t chunk_entry(uint32_t q, uint32_t lg, int pos, uint32_t slab) {
-    return q | lg << 8 | static_cast<uint32_t>(pos + 8) << 10 | slab << 15;
-}
-
-__global__ __launch_bounds__(kBlock) void k_pack_chunk(ChunkArgs a, uint8_t* __restrict__ wire, uint64_t n,
-                                                       uint64_t ntiles);
-__global__ __launch_bounds__(kBlock) void k_unpack_chunk(ChunkArgs a, const uint8_t* __restrict__ wire, uint64_t n,
-                                                         uint64_t ntiles, srpc_unpack_status* st);
-
 }  // namespace srpc_impl
 
 // The object behind the opaque srpc_plan* of include/srpc_gpu.h.
@@ -161,23 +138,9 @@ struct srpc_plan {
     uint32_t ptile_R = 0;            // pack image kernel: records per tile
     size_t ptile_lds = 0;
     size_t tile_lds = 0;
-    int tile_kernel = 0;             // SRPC_TUNE_TILE_KERNEL: 0 LDS image, 1 register-assembled chunks
-    uint8_t* d_chunk = nullptr;      // CHUNK table blob (ChunkArgs::table), nullptr = not eligible
-    uint32_t chunk_table_bytes = 0, chunk_slab_bytes = 0, chunk_P = 0, chunk_rpp = 0, chunk_emax = 0;
-    uint32_t chunk_slab_off[srpc_impl::kMaxFields] = {};
-    int chunk_grid = 0;
-    size_t chunk_lds = 0;
     bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
     srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
     // string schemas (SRPC_PATH_VAR)
     uint32_t nstrings = 0;
     uint32_t fixed_bytes = 0;        // prefix + fixed fields + 8 per string field
-    int var_kernel = 0;              // SRPC_TUNE_VAR_KERNEL: 0 chunk walk (default, per A/B), 1 LDS-staged tiles
-    uint32_t var_tile = 8192;        // SRPC_TUNE_VAR_TILE: staged pack output bytes per tile
-    int var_grid = 0;                // staged pack: resident workgroups (grid-stride over tiles)
 };
-
-namespace srpc_impl {
-// var.hip: size the staged VAR pack grid for the plan's current tile.
-void configure_var(srpc_plan* p);
-}  // namespace srpc_impl

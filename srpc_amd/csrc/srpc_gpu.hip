@@ -482,16 +482,6 @@ __global__ __launch_bounds__(kBlock) void k_fill_splitmix(FillArgs a, uint32_t n
 namespace {
 using namespace srpc_impl;
 
-// TILE kernel default: the LDS-image kernels.  The register-assembled CHUNK
-// kernels (chunk.hip) are parity-tested alternates behind
-// SRPC_TUNE_TILE_KERNEL; on MI355X they lose on pack (square request 207-236
-// vs 188 us) and tie on unpack within the box's noise
-// (profiles/r01_tile_chunk_ab.log).
-#ifndef SRPC_TILE_KERNEL_DEFAULT
-#define SRPC_TILE_KERNEL_DEFAULT 0
-#endif
-constexpr int kDefaultTileKernel = SRPC_TILE_KERNEL_DEFAULT;
-
 template <int W, int ITER, int NT>
 int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, int max_grid, hipStream_t s) {
     const uint64_t per = static_cast<uint64_t>(kBlock) * ITER;
@@ -701,100 +691,6 @@ void configure_tile(srpc_plan* p, uint32_t target) {
     p->tile_full_grid = true;
 }
 
-// CHUNK kernel table for the current tile geometry (chunk.hip): per phase of
-// the period L = lcm(stride, 16) -- the constant chunk bytes, the prefix
-// mask, and the field occurrences.  Plans whose table or slabs do not fit
-// the LDS budget keep the image kernels only.
-void free_chunk(srpc_plan* p) {
-    if (p->d_chunk) {
-        DeviceGuard g(p->device);
-        (void)hipFree(p->d_chunk);
-    }
-    p->d_chunk = nullptr;
-    p->chunk_table_bytes = 0;
-}
-
-int configure_chunk(srpc_plan* p) {
-    free_chunk(p);
-    const uint32_t S = static_cast<uint32_t>(p->stride), R = p->tile_R;
-    const uint32_t L = S / gcd_u32(S, 16) * 16, P = L / 16, rpp = L / S;
-    uint32_t slab = 0;
-    for (uint32_t f = 0; f < p->nfields; ++f) {
-        p->chunk_slab_off[f] = slab;
-        slab += R * p->size[f];  // R is a multiple of 16
-    }
-    std::vector<uint8_t> tmpl(16 * P, 0), pmask(16 * P, 0);
-    std::vector<std::vector<uint32_t>> occ(P);
-    uint32_t emax = 1;
-    for (uint32_t ph = 0; ph < P; ++ph) {
-        for (uint32_t i = 0; i < 16; ++i) {
-            const uint32_t at = (16 * ph + i) % S;
-            if (at < p->prefix_len) {
-                tmpl[16 * ph + i] = p->h_prefix[at];
-                pmask[16 * ph + i] = 0xFF;
-            }
-        }
-        for (uint32_t q = 0; q < rpp; ++q)
-            for (uint32_t f = 0; f < p->nfields; ++f) {
-                const int start = static_cast<int>(q * S + p->off[f]) - static_cast<int>(16 * ph);
-                if (start < 16 && start + static_cast<int>(p->size[f]) > 0)
-                    occ[ph].push_back(chunk_entry(q, ilog2(p->size[f]), start, p->chunk_slab_off[f]));
-            }
-        emax = std::max<uint32_t>(emax, static_cast<uint32_t>(occ[ph].size()));
-    }
-    size_t bytes = 32ull * P + 4ull * P * emax;  // every phase padded to emax entries (0 = none)
-    bytes = (bytes + 15) & ~size_t(15);
-    if (slab >= (1u << 17) || rpp > 255 || slab + bytes > 65536) return SRPC_OK;  // not eligible
-    std::vector<uint8_t> blob(bytes, 0);
-    std::memcpy(blob.data(), tmpl.data(), 16 * P);
-    std::memcpy(blob.data() + 16 * P, pmask.data(), 16 * P);
-    for (uint32_t ph = 0; ph < P; ++ph)
-        std::memcpy(blob.data() + 32 * P + 4ull * ph * emax, occ[ph].data(), 4 * occ[ph].size());
-    p->chunk_emax = emax;
-    DeviceGuard g(p->device);
-    if (hipMalloc(&p->d_chunk, bytes) != hipSuccess) {
-        p->d_chunk = nullptr;
-        return SRPC_E_HIP;
-    }
-    if (hipMemcpy(p->d_chunk, blob.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-        free_chunk(p);
-        return SRPC_E_HIP;
-    }
-    p->chunk_table_bytes = static_cast<uint32_t>(bytes);
-    p->chunk_slab_bytes = slab;
-    p->chunk_P = P;
-    p->chunk_rpp = rpp;
-    p->chunk_lds = slab + bytes;
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_chunk, kBlock, p->chunk_lds) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) {
-        per_cu = 4;
-        cus = 256;
-    }
-    p->chunk_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
-    return SRPC_OK;
-}
-
-ChunkArgs make_chunk_args(const srpc_plan* p, const void* const* cols) {
-    ChunkArgs a{};
-    for (uint32_t f = 0; f < p->nfields; ++f) {
-        a.col[f] = static_cast<const uint8_t*>(cols[f]);
-        a.lg[f] = ilog2(p->size[f]);
-        a.slab_off[f] = p->chunk_slab_off[f];
-    }
-    a.table = p->d_chunk;
-    a.table_bytes = p->chunk_table_bytes;
-    a.slab_bytes = p->chunk_slab_bytes;
-    a.nfields = p->nfields;
-    a.stride = static_cast<uint32_t>(p->stride);
-    a.prefix_len = p->prefix_len;
-    a.R = p->tile_R;
-    a.P = p->chunk_P;
-    a.rpp = p->chunk_rpp;
-    a.emax = p->chunk_emax;
-    return a;
-}
-
 // Device copy of the constant prefix with 16 zero bytes on both sides, so a
 // 16-byte load at any offset in [-15, prefix_len) stays inside the buffer.
 int upload_prefix(srpc_plan* p) {
@@ -882,7 +778,6 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             delete p;
             return SRPC_E_HIP;
         }
-        configure_var(p);
         *out = p;
         return SRPC_OK;
     }
@@ -914,11 +809,6 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             (void)srpc_plan_destroy(p);
             return SRPC_E_HIP;
         }
-        if (configure_chunk(p) != SRPC_OK) {
-            (void)srpc_plan_destroy(p);
-            return SRPC_E_HIP;
-        }
-        p->tile_kernel = p->d_chunk ? kDefaultTileKernel : 0;
     }
     *out = p;
     return SRPC_OK;
@@ -930,7 +820,6 @@ int srpc_plan_destroy(srpc_plan* p) {
         DeviceGuard g(p->device);
         (void)hipFree(p->d_prefix_alloc);
     }
-    free_chunk(p);
     if (p->d_period) {
         DeviceGuard g(p->device);
         (void)hipFree(p->d_period);
@@ -986,26 +875,10 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
     case SRPC_TUNE_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_tile(p, static_cast<uint32_t>(value));
-        if (int rc = configure_chunk(p)) return rc;
-        if (!p->d_chunk) p->tile_kernel = 0;
         return SRPC_OK;
     case SRPC_TUNE_PACK_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_pack_tile(p, static_cast<uint32_t>(value));
-        return SRPC_OK;
-    case SRPC_TUNE_VAR_KERNEL:
-        if ((value != 0 && value != 1) || !p->has_string) return SRPC_E_INVALID;
-        p->var_kernel = value;
-        return SRPC_OK;
-    case SRPC_TUNE_VAR_TILE:
-        if (value < 4096 || value > 32768 || value % 4096 || !p->has_string) return SRPC_E_INVALID;
-        p->var_tile = static_cast<uint32_t>(value);
-        configure_var(p);
-        return SRPC_OK;
-    case SRPC_TUNE_TILE_KERNEL:
-        if (value != 0 && value != 1) return SRPC_E_INVALID;
-        if (value == 1 && !p->d_chunk) return SRPC_E_UNSUPPORTED;
-        p->tile_kernel = value;
         return SRPC_OK;
     default: return SRPC_E_INVALID;
     }
@@ -1028,13 +901,6 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
         DwordVariant v = p->dv;
         v.rpl = x4 ? 4 : 1;
         return launch_dword_any(true, m, wire, n, static_cast<uint32_t>(p->stride / 4), v, s);
-    }
-    const uint64_t ntiles = (n + p->tile_R - 1) / p->tile_R;
-    if (p->tile_kernel == 1) {
-        const ChunkArgs c = make_chunk_args(p, cols);
-        const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->chunk_grid));
-        launch(k_pack_chunk, dim3(grid), dim3(kBlock), static_cast<uint32_t>(p->chunk_lds), s, c, wire, n, ntiles);
-        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     const TileArgs a = make_tile_args(p, cols, true);
     const uint64_t ptiles = (n + p->ptile_R - 1) / p->ptile_R;
@@ -1086,14 +952,6 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         return rc ? rc : ret;
     }
     const uint64_t ntiles = (n_fit + p->tile_R - 1) / p->tile_R;
-    if (p->tile_kernel == 1) {
-        const ChunkArgs c = make_chunk_args(p, reinterpret_cast<const void* const*>(cols));
-        const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->chunk_grid));
-        launch(k_unpack_chunk, dim3(grid), dim3(kBlock), static_cast<uint32_t>(p->chunk_lds), s, c, wire, n_fit,
-               ntiles, st);
-        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
-        return ret;
-    }
     const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     launch(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);

@@ -101,30 +101,6 @@ struct FirstOnly {
     }
 };
 
-// Staged pack (k_pack_var_staged): the tile's first record and, per string
-// field, the index of the first char of that field whose wire byte is at or
-// after the tile start (record `i` starts at `start`; the tile at `pos`).
-// The chars of field f that land in tile t are then exactly
-// [c_lo(t), c_lo(t + 1)): the char -> wire position map is increasing.
-struct FirstAndChars {
-    template <class F>
-    __device__ void operator()(const F& f, uint64_t i, uint64_t start, uint64_t pos, uint64_t* out) const {
-        const VarArgs& a = f.a;
-        out[0] = i;
-        uint64_t w = start + a.prefix_len;
-        for (uint32_t k = 0; k < a.nfields; ++k) {
-            if (a.size[k]) {
-                w += a.size[k];
-                continue;
-            }
-            const uint64_t b0 = a.soff[k][i], len = a.soff[k][i + 1] - b0;
-            w += 8;  // chars begin at w
-            out[1 + a.sidx[k]] = b0 + min(len, pos > w ? pos - w : 0);
-            w += len;
-        }
-    }
-};
-
 __device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t x) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -474,290 +450,6 @@ __global__ __launch_bounds__(kBlock) void k_pack_var(VarArgs a, const uint64_t* 
         }
         __syncthreads();  // the window is rewritten for the next tile
         PHASE(5);
-        PHASE_COUNT(6);
-    }
-    PHASE_END
-}
-
-// ---- staged pack (SRPC_TUNE_VAR_KERNEL 1; slower than the walk on MI355X, kept as an A/B arm) ----
-// The chunk walk above issues one dependent global load per record segment
-// (the walk is 72 % of its time, profiles/r01_var_pack_phases.log).  Here a
-// workgroup owns a T-byte output tile and first copies every source byte the
-// tile needs into LDS: the record window rec_offs[r0..rz+1], each string
-// field's offsets window, each fixed column's [r0, rz] slice, and each string
-// field's chars that land in the tile -- [c_lo(t), c_lo(t+1)), both read from
-// the scan's tile metadata (FirstAndChars), so no staged load depends on
-// another staged byte.  The copies are LDS-DMA (global_load_lds_dwordx4):
-// the regions' aligned 16-byte chunks are numbered one after another and
-// chunk c lands at stage + 16 c, so each wave instruction writes 1 KiB of LDS
-// lane-linearly and no VGPR holds staged data.  Wave 0 builds the region
-// table (one lane per region, a wavefront scan for the chunk numbering) from
-// metadata it prefetched while the previous tile was in flight.  Every lane
-// then assembles 16-byte output chunks from LDS only -- per record segment
-// three aligned 8-byte LDS reads and a funnel shift, merged under a byte
-// mask -- and stores them.
-//
-// A staged chunk is the aligned 16-byte granule holding valid bytes, so it may
-// read up to 15 bytes beyond a source range: always inside that granule, so
-// inside a page the range itself occupies (never a fault); those bytes are
-// masked out and never reach the wire.
-struct StagedLayout {  // LDS byte offsets, all multiples of 16 (host: staged_layout)
-    uint32_t pre;      // the prefix at pre + 16, 16 zero bytes each side
-    uint32_t rtab;     // Region table
-    uint32_t fbase;    // per field u32: fixed -> LDS offset of record r0's value; string -> of its offsets entry r0
-    uint32_t cdelta;   // per field i64: string -> LDS offset of char index x is cdelta + x
-    uint32_t hdr;      // u64: [0] record-window LDS offset, [1] records in the tile, [2] staged chunks
-    uint32_t ctab;     // u16 per 16-byte chunk of the tile: its first record (window index)
-    uint32_t stage;    // staged chunks from stage + 16 (16 bytes of pad before, 32 after)
-    uint32_t cmax;     // staged chunks per tile, upper bound
-    uint32_t total;
-    uint32_t tile;     // T, output bytes per tile (multiple of 16)
-    uint32_t wmax;     // window entries: records per tile + 1 <= T / fixed_bytes + 3
-    uint32_t nregions; // 1 + 2 nstrings + nfixed (<= 64: one wave-0 lane each)
-};
-
-struct Region {        // one staged source range of the current tile
-    uint64_t a;        // 16-aligned source address of its first staged chunk
-    uint32_t c0;       // its first chunk number
-    uint32_t pad;
-};
-
-__host__ __device__ inline uint32_t round16u(uint64_t b) { return static_cast<uint32_t>((b + 15) & ~15ull); }
-// Chunks of a range of at most `bytes` valid bytes at any alignment.
-__host__ __device__ inline uint32_t range_chunks(uint64_t bytes) { return static_cast<uint32_t>((bytes + 30) >> 4); }
-
-typedef const uint8_t __attribute__((address_space(1))) global_u8;
-typedef uint8_t __attribute__((address_space(3))) lds_u8;
-
-// Chunk bytes [b, b + k) := LDS bytes [p, p + k) (1 <= k, b + k <= 16): three
-// aligned 8-byte reads covering [p - b, p - b + 16) and a funnel shift.
-__device__ __forceinline__ void merge_lds(uint64_t& olo, uint64_t& ohi, const uint8_t* lds, uint32_t p, uint32_t b,
-                                          uint32_t k) {
-    const uint32_t x = p - b, sh = 8 * (x & 7u);
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + (x & ~7u));
-    const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-    const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
-    const uint32_t e = b + k;
-    const uint64_t mlo = (b < 8 ? ~0ull << (8 * b) : 0) & (e >= 8 ? ~0ull : (1ull << (8 * e)) - 1);
-    const uint64_t mhi = (e > 8 ? (e >= 16 ? ~0ull : (1ull << (8 * (e - 8))) - 1) : 0) &
-                         (b > 8 ? ~0ull << (8 * (b - 8)) : ~0ull);
-    olo |= lo & mlo;
-    ohi |= hi & mhi;
-}
-
-// Chunk bytes [b, b + k) := the low k bytes of v (k <= 8).
-__device__ __forceinline__ void merge_val(uint64_t& olo, uint64_t& ohi, uint64_t v, uint32_t b, uint32_t k) {
-    if (k < 8) v &= (1ull << (8 * k)) - 1;
-    if (b < 8) {
-        olo |= v << (8 * b);
-        if (b) ohi |= v >> (64 - 8 * b);
-    } else {
-        ohi |= v << (8 * (b - 8));
-    }
-}
-
-// Tile metadata wave 0 needs for one tile, prefetched a tile ahead: the first
-// and last records and, on a chars lane, that string field's char range.
-struct TileMeta {
-    uint64_t r0, rz, clo, chi;
-};
-
-__device__ __forceinline__ TileMeta load_tile_meta(const VarArgs& a, const uint64_t* meta, uint64_t n,
-                                                   uint64_t total, uint64_t T, uint64_t t, int chars_si,
-                                                   uint32_t chars_f) {
-    const uint32_t ms = 1 + a.nstrings;
-    const bool last = (t + 1) * T >= total;
-    const uint64_t* m0 = meta + t * ms;
-    const uint64_t* m1 = meta + (t + 1) * ms;
-    TileMeta M;
-    M.r0 = m0[0];
-    M.rz = last ? n - 1 : max(m1[0], M.r0);
-    M.clo = M.chi = 0;
-    if (chars_si >= 0) {
-        M.clo = m0[1 + chars_si];
-        M.chi = last ? a.soff[chars_f][n] : m1[1 + chars_si];
-    }
-    return M;
-}
-
-__global__ __launch_bounds__(kBlock) void k_pack_var_staged(VarArgs a, StagedLayout L,
-                                                            const uint64_t* __restrict__ rec_offs, uint64_t n,
-                                                            const uint64_t* __restrict__ meta,
-                                                            uint8_t* __restrict__ wire, uint64_t wire_cap,
-                                                            srpc_unpack_status* st) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    Region* rt = reinterpret_cast<Region*>(lds + L.rtab);
-    uint32_t* fb = reinterpret_cast<uint32_t*>(lds + L.fbase);
-    int64_t* cd = reinterpret_cast<int64_t*>(lds + L.cdelta);
-    uint64_t* hdr = reinterpret_cast<uint64_t*>(lds + L.hdr);
-    uint16_t* ctab = reinterpret_cast<uint16_t*>(lds + L.ctab);
-    const uint32_t P = a.prefix_len;
-    for (uint32_t i = threadIdx.x; i < round16u(P) + 32; i += kBlock)
-        lds[L.pre + i] = (i >= 16 && i - 16 < P) ? a.prefix[i - 16] : 0;
-    const uint64_t total = rec_offs[n];
-    const uint64_t limit = min(total, wire_cap);
-    if (total > wire_cap && blockIdx.x == 0 && threadIdx.x == 0 && st)
-        report_bad(st, SRPC_STATUS_BOUNDS, upper_index(rec_offs, n, wire_cap));
-    const uint64_t T = L.tile;
-    const uint64_t ntiles = (limit + T - 1) / T;
-    const uint32_t ns = a.nstrings, nfixed = a.nfields - ns;
-    // wave-0 lane g owns region g: 0 record window, 1..ns offsets windows,
-    // then the fixed columns, then the chars of each string field
-    const uint32_t g = threadIdx.x;
-    const bool region_lane = g < L.nregions;
-    int chars_si = -1;
-    uint32_t field = 0;
-    if (region_lane && g >= 1 + ns + nfixed) chars_si = static_cast<int>(g - 1 - ns - nfixed);
-    if (region_lane && g >= 1 && g <= ns) field = a.sfield[g - 1];
-    else if (region_lane && g > ns && g <= ns + nfixed) field = a.ffield[g - 1 - ns];
-    else if (chars_si >= 0) field = a.sfield[chars_si];
-    TileMeta M{};
-    if (region_lane && blockIdx.x < ntiles)
-        M = load_tile_meta(a, meta, n, total, T, blockIdx.x, chars_si, field);
-    PHASE_BEGIN
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint64_t lo = t * T, hi = min(lo + T, limit);
-        // 1. region table (wave 0, one lane per region), then prefetch the next tile's metadata
-        if (threadIdx.x < 64) {
-            uint64_t rz = M.rz;
-            if (rz - M.r0 + 2 > L.wmax) {  // cannot happen: every record has >= fixed_bytes bytes
-                if (st && g == 0) report_bad(st, SRPC_STATUS_BOUNDS, M.r0);
-                rz = M.r0 + L.wmax - 2;
-            }
-            uint64_t rlo = 0, rhi = 0;
-            if (region_lane) {
-                if (g == 0) {
-                    rlo = reinterpret_cast<uint64_t>(rec_offs + M.r0);
-                    rhi = reinterpret_cast<uint64_t>(rec_offs + rz + 2);
-                } else if (g <= ns) {
-                    rlo = reinterpret_cast<uint64_t>(a.soff[field] + M.r0);
-                    rhi = reinterpret_cast<uint64_t>(a.soff[field] + rz + 2);
-                } else if (chars_si < 0) {
-                    const uint32_t sz = a.size[field];
-                    rlo = reinterpret_cast<uint64_t>(a.col[field] + M.r0 * sz);
-                    rhi = reinterpret_cast<uint64_t>(a.col[field] + (rz + 1) * sz);
-                } else {
-                    rlo = reinterpret_cast<uint64_t>(a.col[field] + M.clo);
-                    rhi = reinterpret_cast<uint64_t>(a.col[field] + max(M.clo, M.chi));
-                }
-            }
-            const uint64_t A = rlo & ~15ull;
-            const uint32_t nch = rhi > rlo ? static_cast<uint32_t>((rhi - A + 15) >> 4) : 0;
-            const uint32_t inc = static_cast<uint32_t>(wave_inclusive_scan(nch));
-            const uint32_t c0 = inc - nch;
-            const uint32_t at = L.stage + 16 + 16 * c0;  // LDS offset of the region's first chunk
-            if (region_lane) {
-                rt[g].a = A;
-                rt[g].c0 = c0;
-                const uint32_t first = at + static_cast<uint32_t>(rlo - A);
-                if (g == 0) {
-                    hdr[0] = first;
-                    hdr[1] = rz - M.r0 + 1;
-                } else if (chars_si < 0) {
-                    fb[field] = first;
-                } else {
-                    cd[field] = static_cast<int64_t>(at) - static_cast<int64_t>(A - reinterpret_cast<uint64_t>(a.col[field]));
-                }
-            }
-            if (g == 63) hdr[2] = min(inc, L.cmax);
-            const uint64_t tn = t + gridDim.x;
-            if (region_lane && tn < ntiles) M = load_tile_meta(a, meta, n, total, T, tn, chars_si, field);
-        }
-        PHASE(0);
-        __syncthreads();
-        PHASE(1);
-        // 2. LDS-DMA staging: chunk c of the tile -> stage + 16 + 16 c
-        const uint32_t C = static_cast<uint32_t>(hdr[2]);
-        for (uint32_t base = 0; base < C; base += kBlock) {
-            const uint32_t c = base + threadIdx.x;
-            if (c < C) {
-                uint32_t r = 0;
-                while (r + 1 < L.nregions && rt[r + 1].c0 <= c) ++r;
-                const uint64_t src = rt[r].a + 16ull * (c - rt[r].c0);
-                const uint32_t wave_c0 = __builtin_amdgcn_readfirstlane(base + (threadIdx.x & ~63u));
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src),
-                                                 (lds_u8*)(lds + L.stage + 16 + 16 * wave_c0), 16, 0,
-                                                 0);
-            }
-        }
-        PHASE(2);
-        __syncthreads();  // waits for the LDS-DMA (vmcnt(0)) and publishes the staged tile
-        PHASE(3);
-        // 3. chunk -> first record table
-        const uint32_t wb = static_cast<uint32_t>(hdr[0]);
-        const uint32_t nrec = static_cast<uint32_t>(hdr[1]);
-        const uint64_t* win = reinterpret_cast<const uint64_t*>(lds + wb);
-        const uint32_t nct = static_cast<uint32_t>((hi - lo + 15) >> 4);
-        for (uint32_t k = threadIdx.x; k < nrec; k += kBlock) {
-            const uint64_t rs = win[k], re = win[k + 1];
-            const uint32_t ca = rs > lo ? static_cast<uint32_t>(min<uint64_t>((rs - lo + 15) >> 4, nct)) : 0;
-            const uint32_t cz = re > lo ? static_cast<uint32_t>(min<uint64_t>((re - lo + 15) >> 4, nct)) : 0;
-            for (uint32_t c = ca; c < cz; ++c) ctab[c] = static_cast<uint16_t>(k);
-        }
-        __syncthreads();
-        PHASE(4);
-        // 4. assemble 16-byte chunks from LDS and store them
-        for (uint32_t c = threadIdx.x; c < nct; c += kBlock) {
-            const uint64_t p0 = lo + 16ull * c;
-            const uint32_t nb = static_cast<uint32_t>(min<uint64_t>(16, hi - p0));
-            uint64_t olo = 0, ohi = 0;
-            uint32_t b = 0, k = ctab[c];
-            uint64_t p = p0;
-            while (b < nb && k < nrec) {
-                const uint64_t rs = win[k], re = win[k + 1];
-                uint64_t q = p - rs;
-                const uint64_t end = q + min<uint64_t>(nb - b, re - p);
-                if (q < P) {
-                    const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(end, P) - q);
-                    merge_lds(olo, ohi, lds, L.pre + 16 + static_cast<uint32_t>(q), b, kk);
-                    b += kk;
-                    q += kk;
-                }
-                uint64_t s = P;
-                for (uint32_t f = 0; f < a.nfields && q < end; ++f) {
-                    const uint32_t sz = a.size[f];
-                    if (sz) {
-                        if (q < s + sz) {
-                            const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(end, s + sz) - q);
-                            merge_lds(olo, ohi, lds, fb[f] + k * sz + static_cast<uint32_t>(q - s), b, kk);
-                            b += kk;
-                            q += kk;
-                        }
-                        s += sz;
-                        continue;
-                    }
-                    const uint64_t* sw = reinterpret_cast<const uint64_t*>(lds + fb[f]) + k;
-                    const uint64_t b0 = sw[0], len = sw[1] - b0;
-                    if (q < s + 8) {
-                        const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(end, s + 8) - q);
-                        merge_val(olo, ohi, len >> (8 * (q - s)), b, kk);
-                        b += kk;
-                        q += kk;
-                    }
-                    s += 8;
-                    if (q < end && q < s + len) {
-                        const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(end, s + len) - q);
-                        merge_lds(olo, ohi, lds, static_cast<uint32_t>(cd[f] + static_cast<int64_t>(b0 + (q - s))), b,
-                                  kk);
-                        b += kk;
-                        q += kk;
-                    }
-                    s += len;
-                }
-                p = rs + q;
-                ++k;
-            }
-            if (nb == 16) {
-                __builtin_nontemporal_store(u64x2{olo, ohi}, reinterpret_cast<u64x2*>(wire + p0));
-            } else {
-                for (uint32_t i = 0; i < nb; ++i)
-                    wire[p0 + i] = static_cast<uint8_t>(i < 8 ? olo >> (8 * i) : ohi >> (8 * (i - 8)));
-            }
-        }
-        PHASE(5);
-        __syncthreads();  // the staged tile and tables are rewritten for the next tile
-        PHASE(7);
         PHASE_COUNT(6);
     }
     PHASE_END
@@ -1284,41 +976,6 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t n
 // ---- host helpers -------------------------------------------------------------
 uint64_t scan_blocks(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 
-constexpr uint32_t kMaxStagedLds = 65536;   // larger layouts fall back to the chunk walk
-constexpr uint64_t kStagedMaxGrid = 1u << 20;
-
-// LDS carve of k_pack_var_staged for output tile T (see StagedLayout).
-StagedLayout staged_layout(const srpc_plan* p, uint32_t T) {
-    StagedLayout L{};
-    L.tile = T;
-    L.wmax = T / p->fixed_bytes + 3;
-    const uint32_t nfixed = p->nfields - p->nstrings;
-    L.nregions = 1 + 2 * p->nstrings + nfixed;
-    uint32_t off = 0;
-    L.pre = off;
-    off += round16u(p->prefix_len) + 32;
-    L.rtab = off;
-    off += round16u(sizeof(Region) * L.nregions);
-    L.fbase = off;
-    off += round16u(4 * p->nfields);
-    L.cdelta = off;
-    off += round16u(8 * p->nfields);
-    L.hdr = off;
-    off += 32;
-    L.ctab = off;
-    off += round16u(2 * (T / 16));
-    // chunks: the windows, the fixed columns' slices, and the chars (<= T bytes over all string fields)
-    uint32_t c = (1 + p->nstrings) * range_chunks(8ull * L.wmax);
-    for (uint32_t f = 0; f < p->nfields; ++f)
-        if (p->size[f]) c += range_chunks(static_cast<uint64_t>(p->size[f]) * (L.wmax - 1));
-    c += (T + 15 * p->nstrings) / 16 + 2 * p->nstrings;
-    L.cmax = c;
-    L.stage = off;
-    off += 16 + 16 * c + 32;
-    L.total = off;
-    return L;
-}
-
 template <class F, class M = FirstOnly>
 int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* tile_first, uint64_t max_tiles,
                 hipStream_t s, uint64_t tile_bytes = kTileBytes, uint32_t meta_stride = 1,
@@ -1365,15 +1022,12 @@ struct ScratchLayout {
 
 uint64_t round256(uint64_t b) { return (b + 255) & ~255ull; }
 
-// Pack's tile metadata is sized for the smallest staged tile (4 KiB), with
-// 1 + nstrings entries per tile, so tuning SRPC_TUNE_VAR_TILE never needs
-// more scratch; max_tiles covers tile index wire_bytes / T + 1 (the staged
-// kernel reads the metadata of the tile after its last one).
+// max_tiles covers tile index wire_bytes / kTileBytes + 1.
 ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes, bool unpack) {
     ScratchLayout L{};
     L.max_tiles = wire_bytes / kTileBytes + 2;
     L.partial_off = 0;
-    const uint64_t domains = unpack ? p->nstrings : 1 + p->nstrings;
+    const uint64_t domains = unpack ? p->nstrings : 1;
     // one partials array per string field: multi-string unpack scans them all in one launch
     L.tiles_off = round256(8 * (std::max<uint64_t>(1, scan_blocks(n)) + 1) * std::max<uint64_t>(1, domains));
     L.lens_off = L.tiles_off + round256(8 * L.max_tiles * domains);
@@ -1385,18 +1039,6 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
 }
 
 }  // namespace
-
-void configure_var(srpc_plan* p) {
-    const StagedLayout L = staged_layout(p, p->var_tile);
-    int per_cu = 0, cus = 0;
-    DeviceGuard g(p->device);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pack_var_staged, kBlock, L.total) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) {
-        per_cu = 4;
-        cus = 256;
-    }
-    p->var_grid = std::max(1, std::min(per_cu, 8)) * std::max(cus, 1);
-}
 
 }  // namespace srpc_impl
 
@@ -1449,21 +1091,6 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     auto* base = static_cast<uint8_t*>(scratch);
     auto* tiles = reinterpret_cast<uint64_t*>(base + L.tiles_off);
     auto* partial = reinterpret_cast<uint64_t*>(base + L.partial_off);
-    const StagedLayout SL = staged_layout(p, p->var_tile);
-    if (p->var_kernel == 1 && SL.total <= kMaxStagedLds && SL.nregions <= 64) {
-        const uint64_t T = SL.tile;
-        const uint64_t max_tiles = wire_cap / T + 2;
-        int rc = launch_scan<PackSizes, FirstAndChars>(PackSizes{a}, n, partial, rec_offs, tiles, max_tiles, s, T,
-                                                       1 + p->nstrings);
-        if (rc) return rc;
-        if (n == 0) return SRPC_OK;
-        if (!wire) return SRPC_E_INVALID;
-        const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(1, (wire_cap + T - 1) / T),
-                                                 p->var_grid > 0 ? p->var_grid : kStagedMaxGrid);
-        launch(k_pack_var_staged, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), SL.total, s, a, SL, rec_offs, n,
-               tiles, wire, wire_cap, st);
-        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
-    }
     const uint64_t g1 = n / kBlock + 1;
     if (g1 > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     if (n && !wire) return SRPC_E_INVALID;

@@ -132,16 +132,11 @@ class GpuPacker:
 
     def tune(self, records_per_lane: int | None = None, iters: int | None = None,
              nontemporal: int | None = None, tile_bytes: int | None = None,
-             grid: int | None = None, tile_kernel: int | None = None,
-             var_kernel: int | None = None, var_tile: int | None = None,
-             pack_tile_bytes: int | None = None) -> None:
-        """Performance knobs (srpc_plan_tune); output bytes never change.
-        tile_kernel: TILE path kernel, 0 = LDS image, 1 = register-assembled chunks.
-        var_kernel: VAR pack kernel, 0 = chunk walk, 1 = LDS-staged tiles (var_tile bytes each)."""
+             grid: int | None = None, pack_tile_bytes: int | None = None) -> None:
+        """Performance knobs (srpc_plan_tune); output bytes never change."""
         L = _lib.lib()
         for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal), (4, tile_bytes),
-                          (5, grid), (6, tile_kernel), (7, var_kernel), (8, var_tile),
-                          (9, pack_tile_bytes)):
+                          (5, grid), (9, pack_tile_bytes)):
             if val is not None:
                 check(L.srpc_plan_tune(self._h, knob, int(val)), "srpc_plan_tune")
 

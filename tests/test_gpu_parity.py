@@ -26,37 +26,6 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
 DEV = torch.device("cuda:0")
 
 
-@pytest.fixture(params=[0, 1], ids=["image", "chunk"])
-def tile_kernel(request, monkeypatch):
-    """Run a test once per TILE-path kernel: every GpuPacker made in it gets
-    that kernel (plans whose table does not fit keep the image kernel)."""
-    init = GpuPacker.__init__
-
-    def patched(self, *a, **kw):
-        init(self, *a, **kw)
-        if self.record_bytes:
-            try:
-                self.tune(tile_kernel=request.param)
-            except srpc_amd.SrpcError:
-                assert request.param == 1
-    monkeypatch.setattr(GpuPacker, "__init__", patched)
-    return request.param
-
-
-@pytest.fixture(params=[(0, 8192), (1, 8192), (1, 4096), (1, 32768)], ids=["walk", "staged", "staged4k", "staged32k"])
-def var_kernel(request, monkeypatch):
-    """Run a string-schema test once per VAR pack kernel / staged tile size."""
-    init = GpuPacker.__init__
-    kernel, tile = request.param
-
-    def patched(self, *a, **kw):
-        init(self, *a, **kw)
-        if not self.record_bytes:
-            self.tune(var_kernel=kernel, var_tile=tile)
-    monkeypatch.setattr(GpuPacker, "__init__", patched)
-    return request.param
-
-
 def dev(a: np.ndarray) -> "torch.Tensor":
     """numpy -> device tensor with the same bytes (16-byte aligned allocation)."""
     b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
@@ -110,7 +79,7 @@ SIZES = [0, 1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 4096 + 17, 100_00
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
 @pytest.mark.parametrize("n", SIZES)
-def test_quad_pack_unpack_vs_oracle(n, path, tile_kernel):
+def test_quad_pack_unpack_vs_oracle(n, path):
     p = GpuPacker(QUAD)
     assert p.path == SRPC_PATH_DWORD
     p.force_path(path)
@@ -124,7 +93,7 @@ def test_quad_pack_unpack_vs_oracle(n, path, tile_kernel):
 
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
-def test_quad_golden_head_and_edges(golden_dir, path, tile_kernel):
+def test_quad_golden_head_and_edges(golden_dir, path):
     p = GpuPacker(QUAD)
     p.force_path(path)
     cols = oracle.splitmix_columns_i32(4, 4096)
@@ -138,7 +107,7 @@ def test_quad_golden_head_and_edges(golden_dir, path, tile_kernel):
 
 
 @pytest.mark.parametrize("path", [SRPC_PATH_DWORD, SRPC_PATH_TILE])
-def test_number_and_two_numbers(golden_dir, manifest, path, tile_kernel):
+def test_number_and_two_numbers(golden_dir, manifest, path):
     p = GpuPacker(NUMBER)
     p.force_path(path)
     n = manifest["streams"]["number_body_1M"]["records"]
@@ -159,7 +128,7 @@ ALL_KINDS = Schema.of("all_kinds", ("k_bool", "bool"), ("k_i8", "int8"), ("k_cha
 ALL_DT = [np.uint8, np.int8, np.int8, np.int16, np.int32, np.int64]
 
 
-def test_all_kinds_tile(golden_dir, tile_kernel):
+def test_all_kinds_tile(golden_dir):
     p = GpuPacker(ALL_KINDS)
     assert p.path == SRPC_PATH_TILE and p.record_bytes == 17
     z = np.load(os.path.join(golden_dir, "all_kinds_in.npz"))
@@ -174,7 +143,7 @@ def test_all_kinds_tile(golden_dir, tile_kernel):
 
 @pytest.mark.parametrize("n", [1, 7, 16, 17, 333, 4099, 65537])
 @pytest.mark.parametrize("schema", ["all", "i16x3", "i64x2", "i8", "mixed_dword"])
-def test_random_schemas_vs_oracle(n, schema, tile_kernel):
+def test_random_schemas_vs_oracle(n, schema):
     kinds = {"all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
              "i16x3": [oracle.INT16] * 3, "i64x2": [oracle.INT64] * 2, "i8": [oracle.INT8],
              "mixed_dword": [oracle.INT64, oracle.INT32, oracle.INT64]}[schema]
@@ -220,7 +189,7 @@ def test_dword_variants_identical(schema):
 
 # ---- envelopes (Calculator.square) ---------------------------------------------
 
-def test_square_request_envelope(golden_dir, manifest, tile_kernel):
+def test_square_request_envelope(golden_dir, manifest):
     st = manifest["streams"]["square_requests_1M"]
     n = st["records"]
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
@@ -235,7 +204,7 @@ def test_square_request_envelope(golden_dir, manifest, tile_kernel):
     assert read_status(s) == (0, 2**64 - 1)
 
 
-def test_square_response_envelope(golden_dir, manifest, tile_kernel):
+def test_square_response_envelope(golden_dir, manifest):
     st = manifest["streams"]["square_responses_1M"]
     n = st["records"]
     p = GpuPacker.for_response(NUMBER, srpc_amd.RPC_SUCCESS)
@@ -247,7 +216,7 @@ def test_square_response_envelope(golden_dir, manifest, tile_kernel):
 
 
 @pytest.mark.parametrize("bad", [0, 5, 143, 144, 145, 9999])
-def test_request_prefix_mismatch_reported(bad, tile_kernel):
+def test_request_prefix_mismatch_reported(bad):
     n = 10_000
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
     nums = np.arange(n, dtype=np.int32) - 5000
@@ -267,7 +236,7 @@ def test_request_prefix_mismatch_reported(bad, tile_kernel):
     assert np.array_equal(back[0], nums)
 
 
-def test_truncated_wire_bounds(tile_kernel):
+def test_truncated_wire_bounds():
     n = 1000
     p = GpuPacker.for_request(NUMBER, SQUARE_METHOD)
     nums = np.arange(n, dtype=np.int32)
@@ -431,7 +400,7 @@ def _rec_offsets(kinds, offs, n, prefix_len=0):
     return r
 
 
-def test_strings_reference_fixture(golden_dir, var_kernel):
+def test_strings_reference_fixture(golden_dir):
     z = np.load(os.path.join(golden_dir, "multiple_strings_in.npz"))
     kinds = MULTIPLE.kinds
     cols = [z["a1"], z["a2"], z["a3"], z["chars"]]
@@ -472,7 +441,7 @@ def _random_string_batch(kinds, n, rng, maxlen):
 @pytest.mark.parametrize("schema,maxlen,envelope", [
     ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
     ("nested", 64, "response"), ("wide", 24, "request")])
-def test_strings_random_vs_oracle(n, schema, maxlen, envelope, var_kernel):
+def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
     kinds = {"s": [oracle.STRING],
              "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
              "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
@@ -544,7 +513,7 @@ def test_strings_skewed_fields_vs_oracle(n, maxlens):
 
 
 @pytest.mark.parametrize("chars_shift,offs_shift", [(0, 0), (3, 8), (15, 8), (1, 0)])
-def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift, var_kernel):
+def test_strings_unaligned_sources_and_long_strings(chars_shift, offs_shift):
     """Chars columns and offset arrays at any byte / 8-byte alignment, strings
     far longer than a 4 KiB tile, and a tiny-record run (many records per tile)."""
     kinds = [oracle.INT8, oracle.STRING, oracle.INT16]
@@ -605,7 +574,7 @@ def _check_single_string(kinds, back, boffs, wire, n, rec, prefix):
     assert back[f].tobytes() == mc
 
 
-def test_strings_errors(var_kernel):
+def test_strings_errors():
     kinds = [oracle.INT32, oracle.STRING]
     n = 1000
     rng = np.random.default_rng(5)

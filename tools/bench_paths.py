@@ -27,10 +27,6 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="substring filter on case names")
-    ap.add_argument("--tile-kernel", default="0,1",
-                    help="TILE cases: comma list of kernels (0 image, 1 chunk)")
-    ap.add_argument("--var", default="", help="VAR cases: comma list of KERNEL:TILE pack variants "
-                    "(e.g. 0:8192,1:8192,1:16384); default: the plan's default")
     args = ap.parse_args()
 
     import numpy as np
@@ -64,25 +60,11 @@ def main():
         return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(dev)
 
     def fixed_case(name, sch, n, prefix=b"", path=None):
-        p0 = GpuPacker(sch, prefix)
-        if path:
-            p0.force_path(path)
-        if p0.path == srpc_amd.SRPC_PATH_TILE:  # every TILE kernel asked for
-            kernels = [int(k) for k in args.tile_kernel.split(",") if k]
-            for k, tag in ((0, "img"), (1, "chunk")):
-                if k in kernels:
-                    one_fixed(f"{name}_{tag}", sch, n, prefix, path, k)
-        else:
-            one_fixed(name, sch, n, prefix, path, None)
-
-    def one_fixed(name, sch, n, prefix, path, tile_kernel):
         if args.only not in name:
             return
         p = GpuPacker(sch, prefix)
         if path:
             p.force_path(path)
-        if tile_kernel is not None:
-            p.tune(tile_kernel=tile_kernel)
         rng = np.random.default_rng(1)
         cols = []
         for k in sch.kinds:
@@ -142,11 +124,7 @@ def main():
         col_bytes = sum(c.nbytes for c, k in zip(cols, kinds) if k != oracle.STRING)
         str_bytes = total - n * fixed
         alg = col_bytes + str_bytes + 8 * (n + 1) * sum(k == oracle.STRING for k in kinds) + total
-        variants = [tuple(int(x) for x in v.split(":")) for v in args.var.split(",") if v] or [None]
-        for var in variants:
-            label = name if var is None else f"{name}_k{var[0]}t{var[1] // 1024}"
-            if var is not None:
-                p.tune(var_kernel=var[0], var_tile=var[1])
+        for label in (name,):
             wire.fill_(0)
             p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s)
             torch.cuda.synchronize()
