@@ -135,6 +135,7 @@ struct srpc_plan {
     int tile_grid = 0;               // resident workgroups for grid-stride tiles
     bool tile_full_grid = true;      // image kernels: one workgroup per tile
     int tile_lb = 8;                 // pack image kernel: 16-byte column loads in flight per lane
+    int tile_flat_k = 0;             // pack: flat kernel's loads per lane (0 = per-field kernel)
     uint32_t ptile_R = 0;            // pack image kernel: records per tile
     size_t ptile_lds = 0;
     size_t tile_lds = 0;

@@ -351,6 +351,109 @@ __global__ __launch_bounds__(kBlock) void k_pack_tile(TileArgs a, uint8_t* __res
     }
 }
 
+// Multi-field pack with every field's column slice loaded in ONE batch.
+// k_pack_tile walks the fields one after another, so a tile pays one memory
+// round trip per field (6 for the 17-byte all-kinds record: 87 % of its wave
+// cycles stalled, profiles/r02_pmc_before_all_kinds.txt).  Here the tile's
+// 16-byte column chunks of all fields are numbered as one list (field f owns
+// chunks [cs[f], cs[f+1])) and lane t takes chunks t, t + 256, ..., t + 256(K-1):
+// all K loads are in flight before the first scatter, and consecutive lanes
+// still read consecutive chunks of one column (coalesced).  K is sized by the
+// host to the tile's chunk count (<= 256 K).
+struct FieldLds {
+    const uint8_t* col;
+    uint32_t size, lg, off, pad;
+};
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_pack_tile_flat(TileArgs a, uint8_t* __restrict__ wire, uint64_t n,
+                                                           uint64_t ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t T = a.R * a.stride;
+    uint8_t* img = lds;
+    uint8_t* tmpl = lds + T;
+    uint8_t* mask = tmpl + a.L;
+    __shared__ FieldLds fl[kMaxFields];
+    if (a.prefix_len) build_template(a, tmpl, mask);
+    if (threadIdx.x < a.nfields)
+        fl[threadIdx.x] = {a.col[threadIdx.x], a.size[threadIdx.x], a.lgsize[threadIdx.x], a.off[threadIdx.x], 0};
+    __syncthreads();
+
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t rbase = tile * a.R;
+        const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+        // item g -> (field, chunk of its column slice): fields' chunk counts
+        // summed uniformly (the last tile is short), no indexed arrays
+        uint32_t fk[K], ck[K];
+        uint32_t total = 0;
+#pragma unroll
+        for (int u = 0; u < K; ++u) fk[u] = ck[u] = 0;
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+#pragma unroll
+            for (int u = 0; u < K; ++u) {
+                const uint32_t g = threadIdx.x + u * kBlock;
+                if (g >= total) {
+                    fk[u] = f;
+                    ck[u] = g - total;
+                }
+            }
+            total += (nr * a.size[f] + 15) >> 4;
+        }
+        uint4 qq[K];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t g = threadIdx.x + u * kBlock;
+            if (g < total) {
+                const uint32_t f = fk[u], c = ck[u];
+                const uint32_t s = fl[f].size;
+                const uint8_t* src = fl[f].col + rbase * s;
+                if ((c + 1) * 16 <= nr * s) qq[u] = *reinterpret_cast<const uint4*>(src + 16 * c);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t g = threadIdx.x + u * kBlock;
+            if (g >= total) break;
+            const uint32_t f = fk[u], c = ck[u];
+            const uint32_t s = fl[f].size, lg = fl[f].lg, off = fl[f].off;
+            const uint32_t e0 = (16 * c) >> lg;
+            const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+            if ((c + 1) * 16 > nr * s) {  // the column's last, partial chunk: whole elements, bytewise
+                const uint8_t* src = fl[f].col + rbase * s;
+                for (uint32_t e = e0; e < nr; ++e)
+                    for (uint32_t i = 0; i < s; ++i) img[e * a.stride + off + i] = src[e * s + i];
+                continue;
+            }
+            switch (s) {
+            case 1: scatter_chunk<1>(img, qq[u], e0, ne, a.stride, off); break;
+            case 2: scatter_chunk<2>(img, qq[u], e0, ne, a.stride, off); break;
+            case 4: scatter_chunk<4>(img, qq[u], e0, ne, a.stride, off); break;
+            default: scatter_chunk<8>(img, qq[u], e0, ne, a.stride, off); break;
+            }
+        }
+        __syncthreads();
+        uint8_t* dst = wire + rbase * a.stride;
+        const uint32_t tbytes = nr * a.stride;
+        const uint32_t full = tbytes >> 4;
+        for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+            uint4 v = *reinterpret_cast<const uint4*>(img + 16 * c);
+            if (a.prefix_len) {
+                const uint32_t ph = (16 * c) % a.L;
+                v = and_not_or(v, *reinterpret_cast<const uint4*>(mask + ph),
+                               *reinterpret_cast<const uint4*>(tmpl + ph));
+            }
+            __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + 16 * c));
+        }
+        if (threadIdx.x == 0) {
+            for (uint32_t i = full * 16; i < tbytes; ++i) {
+                const uint32_t ph = i % a.L;
+                dst[i] = a.prefix_len && mask[ph] ? tmpl[ph] : img[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_t* __restrict__ wire,
                                                         uint64_t n, uint64_t ntiles,
                                                         srpc_unpack_status* st) {
@@ -481,6 +584,13 @@ __global__ __launch_bounds__(kBlock) void k_fill_splitmix(FillArgs a, uint32_t n
 
 namespace {
 using namespace srpc_impl;
+
+// TILE pack of multi-field records: the flat kernel (all fields' column
+// loads in one batch) unless built with -DSRPC_TILE_PACK_FLAT=0 (A/B).
+#ifndef SRPC_TILE_PACK_FLAT
+#define SRPC_TILE_PACK_FLAT 1
+#endif
+constexpr bool kTilePackFlat = SRPC_TILE_PACK_FLAT != 0;
 
 template <int W, int ITER, int NT>
 int launch_dword_v(bool pack, const DwordMap& m, uint8_t* wire, uint64_t n, int rpl, int max_grid, hipStream_t s) {
@@ -663,9 +773,20 @@ void configure_pack_tile(srpc_plan* p, uint32_t target) {
     const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
     p->ptile_R = R;
     p->ptile_lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
-    uint32_t maxc = 1;
-    for (uint32_t f = 0; f < p->nfields; ++f) maxc = std::max(maxc, (R * p->size[f] + 15) / 16);
+    uint32_t maxc = 1, allc = 0;
+    bool mixed = false;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        maxc = std::max(maxc, (R * p->size[f] + 15) / 16);
+        allc += (R * p->size[f] + 15) / 16;
+        mixed |= p->size[f] != p->size[0];
+    }
     p->tile_lb = maxc <= kBlock ? 1 : maxc <= 2 * kBlock ? 2 : maxc <= 4 * kBlock ? 4 : 8;
+    // flat kernel: all fields' chunks in one batch of K loads per lane, for
+    // records of mixed field widths (17-byte all-kinds pack 125 -> 111 us;
+    // equal widths keep the per-field kernel: Quad on TILE 80 -> 84 us with
+    // the flat one, profiles/r02_tile_flat_ab.log)
+    const uint32_t k = (allc + kBlock - 1) / kBlock;
+    p->tile_flat_k = mixed && kTilePackFlat ? (k <= 1 ? 1 : k <= 2 ? 2 : k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 0) : 0;
 }
 
 void configure_tile(srpc_plan* p, uint32_t target) {
@@ -906,6 +1027,15 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
     const uint64_t ptiles = (n + p->ptile_R - 1) / p->ptile_R;
     const uint32_t pgrid = static_cast<uint32_t>(std::min<uint64_t>(ptiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     const size_t lds = p->ptile_lds;
+    switch (p->tile_flat_k) {
+    case 1: launch(k_pack_tile_flat<1>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 2: launch(k_pack_tile_flat<2>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 4: launch(k_pack_tile_flat<4>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 8: launch(k_pack_tile_flat<8>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    case 16: launch(k_pack_tile_flat<16>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
+    default: break;
+    }
+    if (p->tile_flat_k) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     switch (p->tile_lb) {
     case 1: launch(k_pack_tile<1>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
     case 2: launch(k_pack_tile<2>, dim3(pgrid), dim3(kBlock), lds, s, a, wire, n, ptiles); break;
