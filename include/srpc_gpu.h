@@ -125,6 +125,12 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
                                         (1024..49152), pack and unpack           */
 #define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
+#define SRPC_TUNE_VAR_KERNEL 7       /* VAR pack: 1 = record tiles, one pass (default),
+                                        0 = record-offset scan + output chunk walk */
+#define SRPC_TUNE_VAR_IMAGE_BYTES 8  /* VAR record tiles: LDS image bytes (8192..65536,
+                                        multiple of 16); larger tiles take the walk  */
+#define SRPC_TUNE_VAR_CHARS_BYTES 10 /* VAR record tiles: LDS chars stage bytes
+                                        (0..65536, multiple of 16)                   */
 #define SRPC_TUNE_GRID 5             /* DWORD path: max workgroups (0 = one per
                                         256*iter records; else grid-stride)       */
 int srpc_plan_tune(srpc_plan* plan, int knob, int value);

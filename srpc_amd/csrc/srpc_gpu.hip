@@ -997,6 +997,19 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_tile(p, static_cast<uint32_t>(value));
         return SRPC_OK;
+    case SRPC_TUNE_VAR_KERNEL:
+        if ((value != 0 && value != 1) || !p->has_string) return SRPC_E_INVALID;
+        p->var_kernel = value;
+        return SRPC_OK;
+    case SRPC_TUNE_VAR_IMAGE_BYTES:
+        if (value < 8192 || value > 65536 || value % 16 || !p->has_string) return SRPC_E_INVALID;
+        p->rt_img_cap = static_cast<uint32_t>(value);
+        return SRPC_OK;
+    case SRPC_TUNE_VAR_CHARS_BYTES:
+        if (value < 0 || value > 65536 || value % 16 || !p->has_string) return SRPC_E_INVALID;
+        p->rt_ch_cap = static_cast<uint32_t>(value);
+        p->rt_ch_cap_auto = false;
+        return SRPC_OK;
     case SRPC_TUNE_PACK_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_pack_tile(p, static_cast<uint32_t>(value));

@@ -973,6 +973,312 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t n
         for (uint32_t i = threadIdx.x; i < nflags; i += blockDim.x) bad[16 * i] = 0;
 }
 
+// ---- record-tile pack: one pass over the inputs -------------------------------------
+// k_pack_var_rt: a workgroup owns a tile of 256 consecutive records, one per
+// lane, and moves every byte once:
+//   1. wave 0 builds the tile's staging table: per string field its offsets
+//      window soff[r0 .. r0+nr] and its chars [soff[r0], soff[r0+nr]), per
+//      fixed field its column slice; every range is cut into 16-byte aligned
+//      granules, numbered one after another;
+//   2. the granules go to LDS by LDS-DMA, granule x at stage + 16 x (a granule
+//      may hold up to 15 bytes outside its range, never outside the 16-byte
+//      block of a valid byte: no fault, never used);
+//   3. record r starts at r * fixed_bytes + sum_f (soff[f][r] - soff[f][0])
+//      -- every record has fixed_bytes plus its strings' chars -- so the
+//      wire offsets come from the staged windows with no scan -> rec_offs;
+//   4. each lane writes its record -- prefix, fixed values, u64 lengths,
+//      chars -- into an LDS image of the tile's wire span with exact-width
+//      LDS stores (every image byte has one writer);
+//   5. the image leaves with aligned 16-byte non-temporal stores; the two
+//      16-byte blocks the tile shares with its neighbours are written byte
+//      by byte (own bytes only).
+// A tile whose chars or span do not fit the LDS budget writes its span with
+// the chunk walk instead (emit_record, sources read from global memory).
+// Reference semantics: pack_arg<std::string> (packer.hpp:193-198), records
+// appended back to back (core.hpp:34).
+constexpr uint32_t kRtRegions = 2 * kMaxFields;
+constexpr int kRtBatch = 8;  // staged granule loads in flight per lane
+
+struct RtRegion {
+    uint64_t src;  // 16-aligned global address of the region's first granule
+    uint32_t g0;   // its first granule number
+    uint32_t dst;  // LDS offset of its first granule
+};
+
+struct RtArgs {
+    uint32_t pre_at;     // prefix + 32 zero bytes
+    uint32_t stage_at;   // staged granules (offsets windows, column slices, chars), stage_cap bytes
+    uint32_t img_at;     // image, img_cap bytes
+    uint32_t stage_cap, img_cap;
+};
+constexpr uint32_t kRtWin = ((kBlock + 1) * 8 + 16 + 15) & ~15u;  // an offsets window's granules, at most
+constexpr uint64_t kRtImageMin = kBlock * 32;  // the walk's lane slots live in the image
+constexpr uint64_t kRtImageMax = 65536;
+
+typedef const uint8_t __attribute__((address_space(1))) global_u8;
+typedef uint8_t __attribute__((address_space(3))) lds_u8;
+
+// The k <= 8 low bytes of v at LDS byte d, each byte written once, with the
+// widest naturally aligned stores that fit.
+__device__ __forceinline__ void lds_put_small(uint8_t* lds, uint32_t d, uint64_t v, uint32_t k) {
+    if (k && (d & 1)) {
+        lds[d] = static_cast<uint8_t>(v);
+        v >>= 8;
+        ++d;
+        --k;
+    }
+    if (k >= 2 && (d & 2)) {
+        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
+        v >>= 16;
+        d += 2;
+        k -= 2;
+    }
+    while (k >= 4) {
+        *reinterpret_cast<uint32_t*>(lds + d) = static_cast<uint32_t>(v);
+        v >>= 32;
+        d += 4;
+        k -= 4;
+    }
+    if (k >= 2) {
+        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
+        v >>= 16;
+        d += 2;
+        k -= 2;
+    }
+    if (k) lds[d] = static_cast<uint8_t>(v);
+}
+
+// LDS bytes [s, s + len) -> LDS bytes [d, d + len): aligned dword stores in
+// the body, each built from two aligned dword loads of the source and a byte
+// funnel shift (the load may read up to 3 bytes past the run, inside the LDS
+// allocation, never used).
+__device__ __forceinline__ void lds_copy_run(uint8_t* lds, uint32_t d, uint32_t s, uint32_t len) {
+    while (len && (d & 3)) {
+        lds[d++] = lds[s++];
+        --len;
+    }
+    if (len >= 4) {
+        const uint32_t sa = s & 3;
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(lds + (s - sa));
+        uint32_t* dw = reinterpret_cast<uint32_t*>(lds + d);
+        const uint32_t nd = len >> 2;
+        uint32_t w0 = sw[0];
+        for (uint32_t k = 0; k < nd; ++k) {
+            const uint32_t w1 = sw[k + 1];
+            dw[k] = sa ? __builtin_amdgcn_alignbyte(w1, w0, sa) : w0;
+            w0 = w1;
+        }
+        d += 4 * nd;
+        s += 4 * nd;
+        len &= 3;
+    }
+    while (len--) lds[d++] = lds[s++];
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uint64_t n, uint8_t* __restrict__ wire,
+                                                        uint64_t wire_cap, uint64_t* __restrict__ rec_offs,
+                                                        srpc_unpack_status* st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ RtRegion rt[kRtRegions];
+    __shared__ uint64_t lofs[kBlock + 1];     // local record starts (image positions minus h), [nr] = total
+    __shared__ uint64_t climit[kMaxFields];   // string field: soff[f][n] (end of its chars)
+    __shared__ uint32_t fsw[kMaxFields];      // string ordinal -> LDS offset of its window entry 0
+    __shared__ uint32_t fch[kMaxFields];      // string ordinal -> LDS offset of char soff[f][r0]
+    __shared__ uint32_t ffx[kMaxFields];      // fixed ordinal -> LDS offset of its value of record r0
+    __shared__ uint64_t s_base;
+    __shared__ uint32_t s_ngran, s_fits;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ns = a.nstrings, nfx = a.nfields - a.nstrings;
+    // prefix + 32 zero bytes (emit_record reads 16 bytes at any prefix offset)
+    for (uint32_t i = threadIdx.x; i < a.prefix_len + 32; i += kBlock)
+        lds[L.pre_at + i] = i < a.prefix_len ? a.prefix[i] : 0;
+    for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * kBlock;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
+    // 1. staging table (wave 0, one lane per region): region g's granules
+    // land in the stage in granule order, granule x at stage_at + 16 x
+    if (threadIdx.x < 64) {
+        const uint32_t g = lane;
+        uint64_t lo = 0, hi = 0;
+        uint32_t kind = 0;  // 1 offsets window, 2 chars, 3 fixed column slice
+        uint32_t ord = 0;
+        uint64_t before = 0;  // chars of this string field in the records before the tile
+        if (g < ns) {
+            kind = 1;
+            ord = g;
+            const uint64_t* so = a.soff[a.sfield[g]];
+            lo = reinterpret_cast<uint64_t>(so + r0);
+            hi = reinterpret_cast<uint64_t>(so + r0 + nr + 1);
+            before = so[r0] - so[0];
+        } else if (g < ns + nfx) {
+            kind = 3;
+            ord = g - ns;
+            const uint32_t f = a.ffield[ord];
+            lo = reinterpret_cast<uint64_t>(a.col[f] + r0 * a.size[f]);
+            hi = lo + static_cast<uint64_t>(nr) * a.size[f];
+        } else if (g < 2 * ns + nfx) {
+            kind = 2;
+            ord = g - ns - nfx;
+            const uint32_t f = a.sfield[ord];
+            const uint64_t* so = a.soff[f];
+            lo = reinterpret_cast<uint64_t>(a.col[f] + so[r0]);
+            hi = reinterpret_cast<uint64_t>(a.col[f] + so[r0 + nr]);
+        }
+        // record r starts at r * fixed_bytes + sum over string fields of
+        // (soff[r] - soff[0]): the wire offsets need no scan
+        const uint64_t chars_before = __shfl(wave_inclusive_scan(before), 63, 64);
+        if (g == 0) s_base = r0 * a.fixed_bytes + chars_before;
+        const uint64_t A = lo & ~15ull;
+        uint64_t ng = hi > lo ? (hi - A + 15) >> 4 : 0;
+        uint64_t inc = wave_inclusive_scan(ng);
+        // the chars regions come last: when everything does not fit the stage,
+        // the chars are not staged and the tile takes the global walk
+        const bool fits = 16 * __shfl(inc, 63, 64) <= L.stage_cap;
+        if (!fits) {
+            if (kind == 2) ng = 0;
+            inc = wave_inclusive_scan(ng);
+        }
+        if (kind) {
+            const uint32_t g0 = static_cast<uint32_t>(inc - ng);
+            rt[g] = {A, g0, 0};
+            const uint32_t at = L.stage_at + 16 * g0 + static_cast<uint32_t>(lo - A);
+            if (kind == 1) fsw[ord] = at;
+            else if (kind == 2) fch[ord] = at;
+            else ffx[ord] = at;
+        }
+        if (g == 63) {
+            s_ngran = static_cast<uint32_t>(inc);
+            s_fits = fits;
+        }
+    }
+    __syncthreads();
+    // 2. granules -> stage by LDS-DMA (global_load_lds_dwordx4: a wave
+    // instruction fills 1 KiB of LDS lane-linearly, no VGPRs hold the data,
+    // nothing waits until the barrier); a lane's granules increase, so its
+    // region index only moves forward
+    {
+        const uint32_t ngran = s_ngran, nreg = 2 * ns + nfx;
+        uint32_t r = 0;
+        for (uint32_t w0 = threadIdx.x & ~63u; w0 < ngran; w0 += kBlock) {
+            const uint32_t gi = w0 + lane;
+            if (gi < ngran) {
+                while (r + 1 < nreg && rt[r + 1].g0 <= gi) ++r;
+                const uint64_t src = rt[r].src + 16ull * (gi - rt[r].g0);
+                const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src),
+                                                 (lds_u8*)(lds + L.stage_at + 16 * wb), 16, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // waits for the LDS-DMA (vmcnt(0)) and publishes the stage
+    // 3. record starts from the staged offsets windows
+    const uint32_t i = threadIdx.x;
+    if (i < nr) {
+        uint64_t e = static_cast<uint64_t>(i + 1) * a.fixed_bytes;
+        for (uint32_t si = 0; si < ns; ++si) {
+            const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + fsw[si]);
+            e += w[i + 1] - w[0];
+        }
+        lofs[i + 1] = e;
+    }
+    if (i == 0) lofs[0] = 0;
+    __syncthreads();
+    const uint64_t base = s_base, total = lofs[nr];
+    if (i < nr) {
+        const uint64_t start = base + lofs[i], end = base + lofs[i + 1];
+        rec_offs[r0 + i] = start;
+        if (st && start <= wire_cap && wire_cap < end) report_bad(st, SRPC_STATUS_BOUNDS, r0 + i);
+    }
+    if (i == 0 && r0 + nr == n) rec_offs[n] = base + total;
+    const uint32_t h = static_cast<uint32_t>(base & 15);
+    const uint64_t gbase = base & ~15ull;
+    const uint64_t wend = min(base + total, wire_cap);  // wire bytes of this tile end here
+    uint8_t* img = lds + L.img_at;
+    if (s_fits && h + total <= L.img_cap) {
+        // 4. records -> LDS image
+        if (i < nr) {
+            uint32_t d = L.img_at + h + static_cast<uint32_t>(lofs[i]);
+            if (a.prefix_len) {
+                lds_copy_run(lds, d, L.pre_at, a.prefix_len);
+                d += a.prefix_len;
+            }
+            uint32_t si = 0, fi = 0;
+            for (uint32_t f = 0; f < a.nfields; ++f) {
+                const uint32_t sz = a.size[f];
+                if (sz) {
+                    const uint8_t* v = lds + ffx[fi++] + i * sz;
+                    const uint64_t x = sz == 1   ? *v
+                                       : sz == 2 ? load_unaligned<uint16_t>(v)
+                                       : sz == 4 ? load_unaligned<uint32_t>(v)
+                                                 : load_unaligned<uint64_t>(v);
+                    lds_put_small(lds, d, x, sz);
+                    d += sz;
+                    continue;
+                }
+                const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + fsw[si]);
+                const uint64_t c0 = w[0], cb = w[i], len = w[i + 1] - cb;
+                lds_put_small(lds, d, len, 8);
+                d += 8;
+                lds_copy_run(lds, d, fch[si] + static_cast<uint32_t>(cb - c0), static_cast<uint32_t>(len));
+                d += static_cast<uint32_t>(len);
+                ++si;
+            }
+        }
+        __syncthreads();
+        // 5. image -> wire
+        const uint32_t span = h + static_cast<uint32_t>(total);
+        const uint32_t nch = (span + 15) >> 4;
+        for (uint32_t c = threadIdx.x; c < nch; c += kBlock) {
+            const uint64_t g = gbase + 16ull * c;
+            const uint32_t lo = max(h, 16 * c), hi = min(span, 16 * c + 16);
+            if (lo == 16 * c && hi == 16 * c + 16 && g + 16 <= wire_cap) {
+                const u64x2 v = *reinterpret_cast<const u64x2*>(img + 16 * c);
+                __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(wire + g));
+            } else {
+                for (uint32_t x = lo; x < hi && gbase + x < wend; ++x) wire[gbase + x] = img[x];
+            }
+        }
+        return;
+    }
+    // 4'. span or chars too large for LDS: chunk walk over [base, base + total)
+    // with global sources; the image region holds the lanes' 32-byte slots
+    uint32_t f0 = 0;
+    while (a.size[f0]) ++f0;
+    Slot c{img + 32 * threadIdx.x};
+    for (uint64_t p0 = gbase + 16ull * threadIdx.x; p0 < wend; p0 += 16ull * kBlock) {
+        const uint64_t lo = max(p0, base), hi = min(p0 + 16, wend);
+        if (lo >= hi) continue;
+        // last record whose start <= lo (records may be empty)
+        uint32_t k0 = 0, k1 = nr;  // lofs[k0] + base <= lo < lofs[k1] + base
+        while (k1 - k0 > 1) {
+            const uint32_t mid = (k0 + k1) >> 1;
+            if (base + lofs[mid] <= lo) k0 = mid;
+            else k1 = mid;
+        }
+        uint64_t p = lo;
+        uint32_t b = static_cast<uint32_t>(lo - p0);
+        for (uint32_t k = k0; p < hi && k < nr; ++k) {
+            const uint64_t rs = base + lofs[k], re = base + lofs[k + 1];
+            if (re <= p) continue;
+            const uint32_t cnt = static_cast<uint32_t>(min(hi, re) - p);
+            emit_record(a, lds + L.pre_at, climit, f0, nullptr, n, r0 + k, p - rs, cnt, static_cast<int>(b), c);
+            b += cnt;
+            p += cnt;
+        }
+        if (lo == p0 && hi == p0 + 16) {
+            store_slot(wire + p0, c, 16);
+        } else {
+            for (uint64_t x = lo; x < hi; ++x) wire[x] = c.s[x - p0];
+        }
+    }
+}
+
+__global__ void k_zero_u64(uint64_t* p, uint64_t count) {
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        p[i] = 0;
+}
+
 // ---- host helpers -------------------------------------------------------------
 uint64_t scan_blocks(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 
@@ -1038,6 +1344,42 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     return L;
 }
 
+uint32_t round16(uint32_t b) { return (b + 15) & ~15u; }
+
+// LDS carve of k_pack_var_rt (see RtArgs).  The image holds a tile's wire
+// span: 256 records of `avg` bytes (the caller's wire_cap / n, exact when the
+// caller sizes the wire buffer to the batch) with 1/16 slack, unless the plan
+// fixes it (SRPC_TUNE_VAR_IMAGE_BYTES); the stage holds the tile's offsets
+// windows and column slices plus the chars that such a span can hold.  Tiles
+// that do not fit take the chunk walk.
+RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total) {
+    RtArgs L{};
+    uint32_t off = 0;
+    L.pre_at = off;
+    off += round16(p->prefix_len + 32);
+    uint64_t img = p->rt_img_cap;
+    if (!img) {
+        img = std::min<uint64_t>(avg, kRtImageMax) * kBlock;
+        img = std::min<uint64_t>(std::max<uint64_t>(img + img / 16 + 64, kRtImageMin), kRtImageMax);
+    }
+    L.img_cap = round16(static_cast<uint32_t>(img));
+    uint64_t chars = p->rt_ch_cap;
+    if (p->rt_ch_cap_auto) {
+        const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
+        chars = L.img_cap > fixed_span ? L.img_cap - fixed_span : 0;
+    }
+    uint32_t fixed = p->nstrings * kRtWin;
+    for (uint32_t f = 0; f < p->nfields; ++f)
+        if (p->size[f]) fixed += round16(kBlock * p->size[f] + 16);
+    L.stage_cap = fixed + round16(static_cast<uint32_t>(chars)) + 16 * p->nstrings;
+    L.stage_at = off;
+    off += L.stage_cap + 16;  // lds_copy_run may read a dword past a chars run
+    L.img_at = off;
+    off += L.img_cap + 16;
+    *total = off;
+    return L;
+}
+
 }  // namespace
 
 }  // namespace srpc_impl
@@ -1089,6 +1431,25 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     }
     const VarArgs a = make_var_args(p, cols, str_offs);
     auto* base = static_cast<uint8_t*>(scratch);
+    // record tiles, one pass (default) -- unless a tile's span would not fit
+    // the LDS image (records averaging more than ~240 bytes: the scan +
+    // chunk walk below moves long strings at 0.38 of HBM peak, the record
+    // tiles' per-tile walk fallback at 0.10, profiles/r02_var_rt_ab.log)
+    const uint64_t avg = n ? wire_cap / n : 0;
+    if (p->var_kernel == 1 && (p->rt_img_cap || avg * kBlock * 17 / 16 + 64 <= kRtImageMax * 15 / 16)) {
+        if (n == 0) {  // rec_offs[0] = 0
+            launch(k_zero_u64, dim3(1), dim3(64), 0, s, rec_offs, 1ull);
+            return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+        }
+        const uint64_t ntiles = (n + kBlock - 1) / kBlock;
+        if (ntiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        if (!wire) return SRPC_E_INVALID;
+        uint32_t lds = 0;
+        const RtArgs R = rt_layout(p, wire_cap / n, &lds);
+        launch(k_pack_var_rt, dim3(static_cast<uint32_t>(ntiles)), dim3(kBlock), lds, s, a, R, n, wire, wire_cap,
+               rec_offs, st);
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
     auto* tiles = reinterpret_cast<uint64_t*>(base + L.tiles_off);
     auto* partial = reinterpret_cast<uint64_t*>(base + L.partial_off);
     const uint64_t g1 = n / kBlock + 1;

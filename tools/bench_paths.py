@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="substring filter on case names")
+    ap.add_argument("--var-kernel", default="", help="VAR cases: comma list of pack kernels to time "
+                    "(1 record tiles, 0 scan + walk; default: the plan's default)")
+    ap.add_argument("--var-caps", default="", help="VAR record tiles: IMAGE:CHARS bytes (default: the plan's)")
     args = ap.parse_args()
 
     import numpy as np
@@ -124,7 +127,14 @@ def main():
         col_bytes = sum(c.nbytes for c, k in zip(cols, kinds) if k != oracle.STRING)
         str_bytes = total - n * fixed
         alg = col_bytes + str_bytes + 8 * (n + 1) * sum(k == oracle.STRING for k in kinds) + total
-        for label in (name,):
+        if args.var_caps:
+            ib, cb = (int(x) for x in args.var_caps.split(":"))
+            p.tune(var_image_bytes=ib, var_chars_bytes=cb)
+        kernels = [int(k) for k in args.var_kernel.split(",") if k] or [None]
+        for vk in kernels:
+            label = name if vk is None else f"{name}_k{vk}"
+            if vk is not None:
+                p.tune(var_kernel=vk)
             wire.fill_(0)
             p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s)
             torch.cuda.synchronize()
