@@ -75,6 +75,8 @@ typedef enum srpc_kind {
 /* Device-side decode status bits (srpc_unpack_status.flags). */
 #define SRPC_STATUS_PREFIX 1u   /* a record's envelope header != the plan's prefix */
 #define SRPC_STATUS_BOUNDS 2u   /* a record (or string) ran past the wire end      */
+#define SRPC_STATUS_STALLED 4u  /* a tile's offset look-back gave up waiting for an
+                                   earlier tile (never expected; results invalid) */
 
 /* Written by srpc_gpu_unpack when its d_status argument is non-NULL.
  * Reset by the call itself (stream-ordered) before decoding starts. */
@@ -125,8 +127,9 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
                                         (1024..49152), pack and unpack           */
 #define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
-#define SRPC_TUNE_VAR_KERNEL 7       /* VAR pack: 1 = record tiles, one pass (default),
-                                        0 = record-offset scan + output chunk walk */
+#define SRPC_TUNE_VAR_KERNEL 7       /* VAR: 1 = record tiles, one pass (default; unpack of
+                                        multi-string schemas keeps 0), 0 = offset scans +
+                                        chunk walks, 2 = record tiles for every unpack */
 #define SRPC_TUNE_VAR_IMAGE_BYTES 8  /* VAR record tiles: LDS image bytes (8192..65536,
                                         multiple of 16); larger tiles take the walk  */
 #define SRPC_TUNE_VAR_CHARS_BYTES 10 /* VAR record tiles: LDS chars stage bytes

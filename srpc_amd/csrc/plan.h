@@ -145,6 +145,7 @@ struct srpc_plan {
     uint32_t nstrings = 0;
     uint32_t fixed_bytes = 0;        // prefix + fixed fields + 8 per string field
     int var_kernel = 1;              // SRPC_TUNE_VAR_KERNEL: 1 record tiles (one pass), 0 scan + chunk walk
+    bool var_rt_general = false;     // unpack: record tiles with the look-back for multi-string schemas too (A/B)
     uint32_t rt_img_cap = 0;         // record tiles: LDS image bytes, 0 = from wire_cap / n (SRPC_TUNE_VAR_IMAGE_BYTES)
     uint32_t rt_ch_cap = 0;          // record tiles: LDS chars stage bytes (SRPC_TUNE_VAR_CHARS_BYTES)
     bool rt_ch_cap_auto = true;      //   ... or what the image's span can hold

@@ -998,8 +998,9 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         configure_tile(p, static_cast<uint32_t>(value));
         return SRPC_OK;
     case SRPC_TUNE_VAR_KERNEL:
-        if ((value != 0 && value != 1) || !p->has_string) return SRPC_E_INVALID;
-        p->var_kernel = value;
+        if (value < 0 || value > 2 || !p->has_string) return SRPC_E_INVALID;
+        p->var_kernel = value ? 1 : 0;
+        p->var_rt_general = value == 2;
         return SRPC_OK;
     case SRPC_TUNE_VAR_IMAGE_BYTES:
         if (value < 8192 || value > 65536 || value % 16 || !p->has_string) return SRPC_E_INVALID;

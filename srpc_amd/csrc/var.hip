@@ -40,6 +40,7 @@ namespace srpc_impl {
 namespace {
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = static_cast<uint64_t>(kBlock) * kScanItems;  // 2048 items
@@ -653,9 +654,9 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
         const uint32_t sz = a.size[f];
         if (sz) {
             // a fixed field past the record end is never read (it could lie
-            // past the wire buffer): the record is BOUNDS from here on
-            if (flag != SRPC_STATUS_BOUNDS && pos + sz > end) flag = SRPC_STATUS_BOUNDS;
-            if (flag != SRPC_STATUS_BOUNDS) {
+            // past the wire buffer) and its column entry is left unwritten;
+            // the record is then BOUNDS (or stays PREFIX) by the size check below
+            if (flag != SRPC_STATUS_BOUNDS && pos + sz <= end) {
                 uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
                 const uint8_t* q = src + (pos - start);
                 switch (sz) {
@@ -1014,6 +1015,7 @@ struct RtArgs {
 constexpr uint32_t kRtWin = ((kBlock + 1) * 8 + 16 + 15) & ~15u;  // an offsets window's granules, at most
 constexpr uint64_t kRtImageMin = kBlock * 32;  // the walk's lane slots live in the image
 constexpr uint64_t kRtImageMax = 65536;
+constexpr uint64_t kRtuMinAvg = 40;  // record-tile unpack: smallest average record (bytes)
 
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
 typedef uint8_t __attribute__((address_space(3))) lds_u8;
@@ -1273,6 +1275,442 @@ __global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uin
     }
 }
 
+// ---- record-tile unpack: one pass over the wire --------------------------------------
+// k_unpack_var_rt: a workgroup owns 256 consecutive records of the index, one
+// per lane:
+//   1. the tile's index window rec_offs[r0 .. r0+nr] and its wire span
+//      [rec_offs[r0], rec_offs[r0+nr]) go to LDS by LDS-DMA (16-byte
+//      granules, as in k_pack_var_rt);
+//   2. each lane parses its record from the stage (or from global memory when
+//      the record lies outside the staged span: a non-monotonic index, or a
+//      span too large to stage) with the general error semantics of
+//      walk_record: prefix check, fixed fields straight to their columns
+//      (coalesced: lane i writes element r0 + i), every string's length
+//      checked against the record end BEFORE it is used (the reference reads
+//      first: core.hpp:29-31), a BOUNDS record's strings decoded as empty;
+//   3. per string field, a workgroup scan of the lengths gives the chars'
+//      offsets inside the tile, and a decoupled look-back over the tiles'
+//      published chars totals (tile ids from an atomic ticket: every earlier
+//      tile is running and publishes before it looks back) gives the tile's
+//      base -> str_offs;
+//   4. per string field, the lanes copy their chars into an LDS image of the
+//      field's output range, which leaves with aligned 16-byte stores (the
+//      two blocks shared with the neighbouring tiles byte by byte).
+// Reference semantics: pipe_output<T> / pipe_output<std::string>
+// (packer.hpp:210-222) over records appended back to back (core.hpp:34).
+constexpr uint64_t kLookAgg = 1ull << 62, kLookIncl = 2ull << 62, kLookVal = (1ull << 62) - 1;
+#ifndef SRPC_RTU_TICKET
+#define SRPC_RTU_TICKET 0
+#endif
+#ifndef SRPC_RTU_NOLOOK
+#define SRPC_RTU_NOLOOK 0
+#endif
+#ifndef SRPC_RTU_NOCHARS
+#define SRPC_RTU_NOCHARS 0
+#endif
+// Spin budget of one look-back wait (s_sleep 1 per round, ~0.1 s in all):
+// past it the tile gives up, sets SRPC_STATUS_STALLED and uses what it has --
+// a wrong result that is reported, never a hung GPU.
+constexpr uint32_t kLookSpinMax = 1u << 21;
+
+__device__ __forceinline__ uint64_t look_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void look_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Two-level decoupled look-back (wave 0).  look1[t] holds tile t's value
+// (AGG: its own total; INCL: the inclusive prefix); look2[b] the same for
+// blocks of 64 tiles (AGG: the block's total, published by the block's last
+// tile once every tile of the block published its AGG; INCL: the inclusive
+// prefix at the block's end).  Tile t sums its own block's earlier tiles
+// (one round of loads), then whole blocks, 64 per round.  A flat look-back
+// walked back 64 tiles per round until it met an INCL and took 25 us per
+// tile at 2,048 tiles in flight (agent-scope loads pay the Infinity-Cache
+// latency on MI355X, profiles/r02_var_rtu_ab.log); blocks cut that to about
+// two rounds.  Values of one string field, `stride` words apart per tile.
+__device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2, uint64_t t, uint32_t stride,
+                                               uint64_t total, bool* stalled) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = static_cast<uint32_t>(t & 63);
+    const uint64_t blk = t >> 6;
+    uint64_t pre = 0;
+    bool done = false;
+    uint32_t spins = 0;
+    // 1. earlier tiles of the own block, nearest INCL first
+    if (q) {
+        while (true) {
+            const uint64_t v = lane < q ? look_load(look1 + ((blk << 6) + lane) * stride) : kLookAgg;
+            const uint64_t incl = __ballot(lane < q && v >= kLookIncl);
+            const uint32_t from = incl ? 63 - __builtin_clzll(incl) : 0;  // highest INCL lane, or 0
+            const uint64_t wait = __ballot(lane < q && lane >= from && v < kLookAgg);
+            if (wait && ++spins < kLookSpinMax) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            if (wait) *stalled = true;
+            const uint64_t part = (lane < q && lane >= from) ? (v & kLookVal) : 0;
+            pre = __shfl(wave_inclusive_scan(part), 63, 64);
+            done = incl != 0;
+            break;
+        }
+    } else {
+        done = blk == 0;
+    }
+    if (q == 63 && lane == 0)  // the block's total (or already its inclusive prefix)
+        look_store(look2 + blk * stride, (done ? kLookIncl : kLookAgg) | ((pre + total) & kLookVal));
+    // 2. whole blocks before the own block, 64 per round
+    int64_t j = static_cast<int64_t>(blk) - 1;
+    while (!done && j >= 0) {
+        const int64_t idx = j - static_cast<int64_t>(lane);
+        const uint64_t v = idx >= 0 ? look_load(look2 + static_cast<uint64_t>(idx) * stride) : kLookIncl;
+        const uint64_t incl = __ballot(v >= kLookIncl);
+        const uint64_t wait = __ballot(v < kLookAgg);
+        const uint32_t first = incl ? __builtin_ctzll(incl) : 64;
+        const uint64_t upto = first >= 63 ? ~0ull : (2ull << first) - 1;
+        if ((wait & upto) && ++spins < kLookSpinMax) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (wait & upto) *stalled = true;
+        const uint64_t part = lane <= first ? (v & kLookVal) : 0;
+        pre += __shfl(wave_inclusive_scan(part), 63, 64);
+        if (first < 64) break;
+        j -= 64;
+    }
+    if (lane == 0) {
+        look_store(look1 + t * stride, kLookIncl | ((pre + total) & kLookVal));
+        if (q == 63 && !done) look_store(look2 + blk * stride, kLookIncl | ((pre + total) & kLookVal));
+    }
+    return pre;
+}
+
+struct RtuArgs {
+    uint32_t pre_at;     // prefix + 16 bytes
+    uint32_t stage_at;   // index window granules (kRtWin bytes), then the wire span's (stage_cap bytes)
+    uint32_t pos_at;     // per string ordinal: 256 u64 chars positions (wire offsets)
+    uint32_t len_at;     // per string ordinal: 256 u64 lengths, then offsets inside the tile's chars
+    uint32_t img_at;     // chars image, img_cap bytes
+    uint32_t stage_cap, img_cap;
+};
+
+// General decode of record r (walk_record's multi-string semantics); string
+// ordinal si's chars position and length go to pos/len[si * 256 + lane].
+template <typename Pre>
+__device__ __forceinline__ uint32_t parse_record(const VarArgs& a, const uint8_t* src, const Pre* pre, uint64_t r,
+                                                 uint64_t start, uint64_t end, uint64_t wire_len, uint64_t* pos_l,
+                                                 uint64_t* len_l, uint32_t i) {
+    uint32_t flag = 0;
+    if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
+    if (!flag) {
+        uint32_t k = 0;
+        for (; k + 8 <= a.prefix_len; k += 8)
+            if (load_unaligned<uint64_t>(src + k) != load_unaligned<uint64_t>(pre + k)) flag = SRPC_STATUS_PREFIX;
+        for (; k < a.prefix_len; ++k)
+            if (src[k] != pre[k]) flag = SRPC_STATUS_PREFIX;
+    }
+    uint64_t pos = start + a.prefix_len;
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            if (flag != SRPC_STATUS_BOUNDS && pos + sz <= end) {
+                uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
+                const uint8_t* q = src + (pos - start);
+                switch (sz) {
+                case 1: dst[0] = q[0]; break;
+                case 2: *reinterpret_cast<uint16_t*>(dst) = load_unaligned<uint16_t>(q); break;
+                case 4: *reinterpret_cast<uint32_t*>(dst) = load_unaligned<uint32_t>(q); break;
+                default: *reinterpret_cast<uint64_t*>(dst) = load_unaligned<uint64_t>(q); break;
+                }
+            }
+            pos += sz;
+            continue;
+        }
+        uint64_t len = 0;
+        if (flag != SRPC_STATUS_BOUNDS && pos + 8 <= end) {
+            len = load_unaligned<uint64_t>(src + (pos - start));
+            pos += 8;
+            if (len > end - pos) {
+                flag = SRPC_STATUS_BOUNDS;
+                len = 0;
+            }
+        } else {
+            flag = SRPC_STATUS_BOUNDS;
+        }
+        pos_l[si * kBlock + i] = pos;
+        len_l[si * kBlock + i] = len;
+        ++si;
+        pos += len;
+    }
+    if (!flag && pos != end) flag = SRPC_STATUS_BOUNDS;  // record size disagrees with the index
+    if (flag == SRPC_STATUS_BOUNDS)
+        for (uint32_t k = 0; k < a.nstrings; ++k) len_l[k * kBlock + i] = 0;
+    return flag;
+}
+
+// kOpt (single-string schemas): no look-back -- when every record is exact
+// (its decoded string length is its index size minus fixed_bytes), string
+// chars of record r start at rec_offs[r] - rec_offs[0] - r * fixed_bytes, so
+// the tile's base comes from its index window alone.  A tile holding a record
+// that is not exact (or whose base would leave the chars buffer) sets *bad;
+// then the general kernel (kOpt = false, gated on *bad) decodes the whole
+// batch again with the look-back and rewrites every output.
+template <bool kOpt>
+__global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, const uint8_t* __restrict__ wire,
+                                                          uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
+                                                          uint64_t n, uint64_t* __restrict__ look,
+                                                          uint64_t* __restrict__ look2, uint32_t* __restrict__ ticket,
+                                                          srpc_unpack_status* st, uint32_t* __restrict__ bad) {
+    if constexpr (!kOpt)
+        if (bad && *bad == 0) return;  // the optimistic pass was exact everywhere
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ RtRegion rt[2];
+    __shared__ uint64_t s_tile, s_lo, s_hi, s_base, s_first;
+    __shared__ uint32_t s_inexact;
+    __shared__ uint64_t s_tot[kMaxFields], s_pre[kMaxFields];
+    __shared__ uint32_t s_ioff[kMaxFields];
+    __shared__ uint32_t s_ngran, s_staged, s_fits;
+    const uint32_t lane = threadIdx.x & 63, i = threadIdx.x;
+    const uint32_t ns = a.nstrings;
+#if SRPC_RTU_TICKET
+    if (i == 0) s_tile = atomicAdd(ticket, 1u);
+#else
+    // tile = blockIdx.x: every XCD dispatches its workgroups in increasing
+    // order, so the smallest unfinished tile is always resident and every
+    // look-back ends (one ticket atomic per tile, all on one address, cost
+    // ~10 ns each at the memory side: 32K tiles -> 300 us, r02_var_rtu_ab.log);
+    // the spin limit in the look-back guarantees termination regardless
+    if (i == 0) s_tile = blockIdx.x;
+#endif
+    for (uint32_t k = i; k < a.prefix_len + 16; k += kBlock) lds[L.pre_at + k] = k < a.prefix_len ? a.prefix[k] : 0;
+    __syncthreads();
+    const uint64_t t = s_tile;
+    const uint64_t r0 = t * kBlock;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
+    // 1. staging table: region 0 the index window, region 1 the wire span
+    if (i < 64) {
+        uint64_t lo = 0, hi = 0;
+        if (lane == 0) {
+            lo = reinterpret_cast<uint64_t>(rec_offs + r0);
+            hi = reinterpret_cast<uint64_t>(rec_offs + r0 + nr + 1);
+        } else if (lane == 1) {
+            const uint64_t w0 = rec_offs[r0], w1 = rec_offs[r0 + nr];
+            s_lo = w0;
+            s_hi = w1;
+            if (kOpt) {
+                s_first = rec_offs[0];
+                s_inexact = 0;
+            }
+            if (w0 < w1 && w1 <= wire_len) {
+                lo = reinterpret_cast<uint64_t>(wire + w0);
+                hi = reinterpret_cast<uint64_t>(wire + w1);
+            }
+        }
+        const uint64_t A = lo & ~15ull;
+        uint64_t ng = hi > lo ? (hi - A + 15) >> 4 : 0;
+        if (lane == 1 && 16 * ng > L.stage_cap) ng = 0;  // span too large: parse from global memory
+        const uint64_t inc = wave_inclusive_scan(ng);
+        if (lane < 2) {
+            rt[lane] = {A, static_cast<uint32_t>(inc - ng), 0};
+            if (lane == 1) {
+                s_staged = ng != 0;
+                s_base = A - reinterpret_cast<uint64_t>(wire);  // wire offset of the stage's first granule
+            }
+        }
+        if (lane == 63) s_ngran = static_cast<uint32_t>(inc);
+    }
+    __syncthreads();
+    {
+        const uint32_t ngran = s_ngran;
+        uint32_t r = 0;
+        for (uint32_t w0 = i & ~63u; w0 < ngran; w0 += kBlock) {
+            const uint32_t gi = w0 + lane;
+            if (gi < ngran) {
+                if (r == 0 && rt[1].g0 <= gi) r = 1;
+                const uint64_t src = rt[r].src + 16ull * (gi - rt[r].g0);
+                const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src),
+                                                 (lds_u8*)(lds + L.stage_at + 16 * wb), 16, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // waits for the LDS-DMA (vmcnt(0)) and publishes the stage
+    const uint64_t* win = reinterpret_cast<const uint64_t*>(
+        lds + L.stage_at + static_cast<uint32_t>(reinterpret_cast<uint64_t>(rec_offs + r0) & 15));
+    const bool staged = s_staged;
+    const uint64_t slo = s_lo, shi = s_hi;
+    // the wire span's first granule follows the window's granules
+    const uint8_t* sbase = lds + L.stage_at + 16 * rt[1].g0;
+    const uint64_t sw = s_base;  // wire offset of sbase[0]
+    uint64_t* pos_l = reinterpret_cast<uint64_t*>(lds + L.pos_at);
+    uint64_t* len_l = reinterpret_cast<uint64_t*>(lds + L.len_at);
+    // 2. parse
+    if (i < nr) {
+        const uint64_t start = win[i], end = win[i + 1];
+        uint32_t flag;
+        if (staged && start >= slo && end <= shi && start <= end)
+            flag = parse_record(a, sbase + (start - sw), lds + L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
+        else
+            flag = parse_record(a, wire + start, lds + L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
+        if (flag && st) report_bad(st, flag, r0 + i);
+        if (kOpt && (start > end || end - start < a.fixed_bytes || len_l[i] != end - start - a.fixed_bytes))
+            s_inexact = 1;
+    } else {
+        for (uint32_t k = 0; k < ns; ++k) len_l[k * kBlock + i] = 0;
+    }
+    __syncthreads();
+    // 3. per string field: offsets inside the tile, tile totals
+    for (uint32_t si = 0; si < ns; ++si) {
+        uint64_t tot;
+        // lengths become exclusive offsets in place (len = next offset - offset)
+        const uint64_t x = block_exclusive_scan(len_l[si * kBlock + i], &tot);
+        len_l[si * kBlock + i] = x;
+        if (i == 0) {
+            s_tot[si] = tot;
+            if (!kOpt) look_store(look + t * ns + si, (t == 0 ? kLookIncl : kLookAgg) | (tot & kLookVal));
+        }
+    }
+    if (kOpt) {  // the tile's chars base, valid when every record before it is exact
+        if (i == 0) {
+            const uint64_t first = s_first, w0 = win[0];
+            const uint64_t fixed_before = r0 * a.fixed_bytes;
+            const bool ok = !s_inexact && w0 >= first && w0 - first >= fixed_before &&
+                            w0 - first - fixed_before <= wire_len && s_tot[0] <= wire_len - (w0 - first - fixed_before);
+            s_pre[0] = ok ? w0 - first - fixed_before : 0;
+            if (!ok) {
+                atomicOr(bad, 1u);
+                s_inexact = 1;
+            }
+        }
+        __syncthreads();
+        if (s_inexact) return;  // the general pass rewrites this tile
+    }
+    // every field's chars image at local offsets (16 bytes of slack on each
+    // side), independent of the tile's output base: waves 1-3 build theirs
+    // while wave 0 looks back, then wave 0 builds its own
+    if (i == 0) {
+        uint64_t at = 16;
+        for (uint32_t k = 0; k < ns; ++k) {
+            s_ioff[k] = static_cast<uint32_t>(min<uint64_t>(at, 0xffffffffull));
+            at += ((s_tot[k] + 15) & ~15ull) + 16;
+        }
+        s_fits = at + 16 <= L.img_cap;
+    }
+    __syncthreads();
+    const bool fits = s_fits;
+    auto build = [&]() {
+        if (!fits || i >= nr) return;
+        for (uint32_t k = 0; k < ns; ++k) {
+            const uint64_t o = len_l[k * kBlock + i], pos = pos_l[k * kBlock + i];
+            const uint64_t len = (i + 1 < kBlock ? len_l[k * kBlock + i + 1] : s_tot[k]) - o;
+            if (!len) continue;
+            const uint32_t d = L.img_at + s_ioff[k] + static_cast<uint32_t>(o);
+            if (staged && pos >= slo && pos + len <= shi) {
+                lds_copy_run(lds, d, static_cast<uint32_t>(sbase - lds) + static_cast<uint32_t>(pos - sw),
+                             static_cast<uint32_t>(len));
+            } else {
+                for (uint64_t x = 0; x < len; x += 8) {
+                    const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(8, len - x));
+                    uint64_t v = 0;
+                    for (uint32_t b = 0; b < kk; ++b) v |= static_cast<uint64_t>(wire[pos + x + b]) << (8 * b);
+                    lds_put_small(lds, d + static_cast<uint32_t>(x), v, kk);
+                }
+            }
+        }
+    };
+    if (!kOpt && i < 64) {
+        bool stalled = false;
+        for (uint32_t si = 0; si < ns; ++si) {
+#if SRPC_RTU_NOLOOK  // A/B timing only: wrong offsets
+            const uint64_t pre = 0;
+#else
+            const uint64_t pre = t ? look_back2(look + si, look2 + si, t, ns, s_tot[si], &stalled) : 0;
+#endif
+            if (lane == 0) s_pre[si] = pre;
+        }
+        if (stalled && lane == 0 && st) report_bad(st, SRPC_STATUS_STALLED, r0);
+    }
+    build();
+    __syncthreads();
+    // 4. str_offs and chars, per string field; chunk c of the output covers
+    // image bytes [16c - h, 16c + 16 - h), h = the base's offset in its 16-byte
+    // block, the same for every chunk: a uniform byte shift of two aligned
+    // 16-byte image reads
+    uint8_t* img = lds + L.img_at;
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        if (a.size[f]) continue;
+        const uint64_t P = s_pre[si], tot = s_tot[si];
+        uint64_t* so = const_cast<uint64_t*>(a.soff[f]);
+        uint8_t* chars = const_cast<uint8_t*>(a.col[f]);
+        const uint64_t o = len_l[si * kBlock + i];
+        if (i < nr) so[r0 + i] = P + o;
+        if (i == 0 && r0 + nr == n) so[n] = P + tot;
+        const uint32_t h = static_cast<uint32_t>(P & 15);
+        const uint64_t gbase = P & ~15ull;
+        if (fits && !SRPC_RTU_NOCHARS) {
+            const uint8_t* im = img + s_ioff[si];  // local chars x at im[x]; 16 bytes of slack either side
+            const uint32_t span = h + static_cast<uint32_t>(tot);
+            const uint32_t nch = (span + 15) >> 4;
+            const uint32_t sh = (16 - h) & 15;  // (16c - h) mod 16
+            for (uint32_t c = i; c < nch; c += kBlock) {
+                const uint32_t lo = max(h, 16 * c), hi = min(span, 16 * c + 16);
+                if (lo == 16 * c && hi == 16 * c + 16) {
+                    // image bytes [16c - h, 16c - h + 16) = bytes sh.. of the aligned pair at 16c - h - sh
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(im + 16 * c - h - sh);
+                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6],
+                                   w7 = w[7];
+                    uint32_t o0, o1, o2, o3;
+                    const uint32_t b = sh & 3;
+                    switch (sh >> 2) {  // uniform
+                    case 0:
+                        o0 = __builtin_amdgcn_alignbyte(w1, w0, b); o1 = __builtin_amdgcn_alignbyte(w2, w1, b);
+                        o2 = __builtin_amdgcn_alignbyte(w3, w2, b); o3 = __builtin_amdgcn_alignbyte(w4, w3, b);
+                        break;
+                    case 1:
+                        o0 = __builtin_amdgcn_alignbyte(w2, w1, b); o1 = __builtin_amdgcn_alignbyte(w3, w2, b);
+                        o2 = __builtin_amdgcn_alignbyte(w4, w3, b); o3 = __builtin_amdgcn_alignbyte(w5, w4, b);
+                        break;
+                    case 2:
+                        o0 = __builtin_amdgcn_alignbyte(w3, w2, b); o1 = __builtin_amdgcn_alignbyte(w4, w3, b);
+                        o2 = __builtin_amdgcn_alignbyte(w5, w4, b); o3 = __builtin_amdgcn_alignbyte(w6, w5, b);
+                        break;
+                    default:
+                        o0 = __builtin_amdgcn_alignbyte(w4, w3, b); o1 = __builtin_amdgcn_alignbyte(w5, w4, b);
+                        o2 = __builtin_amdgcn_alignbyte(w6, w5, b); o3 = __builtin_amdgcn_alignbyte(w7, w6, b);
+                        break;
+                    }
+                    __builtin_nontemporal_store(u32x4{o0, o1, o2, o3}, reinterpret_cast<u32x4*>(chars + gbase + 16 * c));
+                } else {
+                    for (uint32_t x = lo; x < hi; ++x) chars[gbase + x] = im[x - h];
+                }
+            }
+        } else if (!SRPC_RTU_NOCHARS && i < nr) {  // the tile's chars exceed the image: copied lane by lane
+            const uint64_t pos = pos_l[si * kBlock + i];
+            const uint64_t len = (i + 1 < kBlock ? len_l[si * kBlock + i + 1] : tot) - o;
+            const bool in_stage = staged && pos >= slo && pos + len <= shi;
+            const uint8_t* src = in_stage ? sbase + (pos - sw) : wire + pos;
+            uint8_t* dst = chars + P + o;
+            for (uint64_t k = 0; k < len; ++k) dst[k] = src[k];
+        }
+        ++si;
+    }
+}
+
+__global__ void k_str_offs_zero(VarArgs a) {  // n == 0: str_offs[f][0] = 0
+    const uint32_t f = threadIdx.x;
+    if (f < a.nfields && !a.size[f]) const_cast<uint64_t*>(a.soff[f])[0] = 0;
+}
+
+__global__ void k_zero_u64_gated(uint64_t* p, uint64_t count, const uint32_t* gate) {
+    if (*gate == 0) return;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        p[i] = 0;
+}
+
 __global__ void k_zero_u64(uint64_t* p, uint64_t count) {
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
@@ -1322,7 +1760,7 @@ VarArgs make_var_args(const srpc_plan* p, const void* const* cols, const uint64_
 //   unpack only: [lens: ns*n u64] [spos: ns*n u64]
 // Pack has one tile domain (the wire); unpack one per string field (its chars).
 struct ScratchLayout {
-    uint64_t partial_off, tiles_off, lens_off, spos_off, bad_off, long_off, total;
+    uint64_t partial_off, tiles_off, lens_off, spos_off, bad_off, long_off, look_off, total;
     uint64_t max_tiles;
 };
 
@@ -1340,7 +1778,10 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
     L.spos_off = L.lens_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
     L.bad_off = L.spos_off + (unpack ? round256(8 * static_cast<uint64_t>(p->nstrings) * n) : 0);
     L.long_off = L.bad_off + 64 * kLongFlags;
-    L.total = L.long_off + round256(4 * L.max_tiles);
+    // record-tile unpack: ticket + a look-back word per 256-record tile and string field
+    L.look_off = L.long_off + round256(4 * L.max_tiles);
+    const uint64_t nt = (n + kBlock - 1) / kBlock;
+    L.total = L.look_off + round256(8 * (1 + (nt + (nt + 63) / 64) * p->nstrings));
     return L;
 }
 
@@ -1378,6 +1819,36 @@ RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total) {
     off += L.img_cap + 16;
     *total = off;
     return L;
+}
+
+// LDS carve of k_unpack_var_rt: the stage holds the index window and a
+// tile's wire span (256 records of wire_len / n bytes with 1/16 slack); the
+// chars image one string field's chars of a tile.  Returns false when the
+// span would not fit (long records keep the walk + scans + chars kernels).
+bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total) {
+    RtuArgs L{};
+    const uint64_t span = std::min<uint64_t>(avg, kRtImageMax) * kBlock;
+    const uint64_t cap = span + span / 16 + 64;
+    if (cap > kRtImageMax * 3 / 4) return false;
+    uint32_t off = 0;
+    L.pre_at = off;
+    off += round16(p->prefix_len + 16);
+    L.stage_cap = round16(static_cast<uint32_t>(cap));
+    L.stage_at = off;
+    off += kRtWin + L.stage_cap + 16;  // lds_copy_run may read a dword past a run
+    L.pos_at = off;
+    off += 8 * kBlock * p->nstrings;
+    L.len_at = off;
+    off += 8 * kBlock * p->nstrings;
+    const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
+    // every string field's chars of a tile, 16 bytes of slack around each
+    L.img_cap = round16(static_cast<uint32_t>(std::max<uint64_t>(1024, cap > fixed_span ? cap - fixed_span : 0) +
+                                              32 * (p->nstrings + 1)));
+    L.img_at = off;
+    off += L.img_cap + 32;
+    *out = L;
+    *total = off;
+    return true;
 }
 
 }  // namespace
@@ -1522,6 +1993,41 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     const uint64_t grid = (n + kBlock - 1) / kBlock;
     if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     auto* bad = reinterpret_cast<uint32_t*>(base + L.bad_off);
+    // record tiles, one pass (default), for batches whose tiles' wire spans fit LDS
+    RtuArgs R{};
+    uint32_t rlds = 0;
+    // (single-string schemas; multi-string batches keep the walk + scans +
+    // chars kernels: a look-back on the tiles' chars totals made the record
+    // tiles no faster there, profiles/r02_var_rtu_ab.log)
+    // Very short records (under ~40 bytes on average) keep the staged walk +
+    // chars kernels as well: their 256-record tiles are too small to pay for a
+    // tile's fixed cost (0-16 B strings 104 vs 142 us, 0-32 B 71 vs 88 us;
+    // 50-byte records 206 -> 146 us with the tiles, profiles/r02_var_rtu_ab.log).
+    if (p->var_kernel == 1 && (p->nstrings == 1 || p->var_rt_general) &&
+        (n == 0 || ((wire_len / n >= kRtuMinAvg || p->var_rt_general) && rtu_layout(p, wire_len / n, &R, &rlds)))) {
+        if (n == 0) {
+            launch(k_str_offs_zero, dim3(1), dim3(64), 0, s, a);
+            return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+        }
+        if (!wire) return SRPC_E_INVALID;
+        auto* look = reinterpret_cast<uint64_t*>(base + L.look_off);
+        // ticket + look-back words per tile and per 64-tile block, per string field
+        const uint64_t w1 = grid * p->nstrings, w2 = ((grid + 63) / 64) * p->nstrings;
+        const uint64_t words = 1 + w1 + w2;
+        const uint32_t zgrid = static_cast<uint32_t>(std::min<uint64_t>((words + 255) / 256, 1024));
+        if (p->nstrings == 1) {
+            launch(k_zero_u64, dim3(1), dim3(64), 0, s, reinterpret_cast<uint64_t*>(bad), 1ull);
+            launch(k_unpack_var_rt<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
+                   wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad);
+            launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
+        } else {
+            launch(k_zero_u64, dim3(zgrid), dim3(256), 0, s, look, words);
+        }
+        launch(k_unpack_var_rt<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire, wire_len,
+               rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st,
+               p->nstrings == 1 ? bad : nullptr);
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
     if (p->nstrings == 1 && n) {  // single-string fast path: no scan unless a record is not exact
         if (!wire) return SRPC_E_INVALID;
         const uint32_t f = a.sfield[0];

@@ -672,9 +672,8 @@ def _model_multi_string(kinds, wire: bytes, n, rec, prefix: bytes):
         for f, k in enumerate(kinds):
             if k != oracle.STRING:
                 sz = oracle.KIND_SIZE[k]
-                if flag != srpc_amd.SRPC_STATUS_BOUNDS and pos + sz > end:
-                    flag = srpc_amd.SRPC_STATUS_BOUNDS  # never read past the record end
-                if flag != srpc_amd.SRPC_STATUS_BOUNDS:
+                # a field past the record end is not decoded (the size check flags the record)
+                if flag != srpc_amd.SRPC_STATUS_BOUNDS and pos + sz <= end:
                     vals[(f, r)] = bytes(wire[pos:pos + sz])
                 pos += sz
                 continue
