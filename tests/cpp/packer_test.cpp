@@ -234,6 +234,27 @@ static void test_bodies_and_bounds() {
     int32_t v = 7;
     q >> v;
     CHECK(!q.ok() && v == 0);
+    // a request cut at every length, and oversized string lengths: the
+    // hardened reads flag the buffer and never read past it (run under
+    // ASan/UBSan by tests/test_sanitizers.py; the reference reads first and
+    // checks after, packer.hpp:212-213)
+    register_test_messages();
+    const std::vector<uint8_t> whole = packed_request(make_nm(), "test");
+    int cut_ok = 0;
+    for (size_t cut = 0; cut < whole.size(); ++cut) {
+        packer pr(std::vector<uint8_t>(whole.begin(), whole.begin() + static_cast<long>(cut)));
+        auto r = pr.unpack_request<nested_message>();
+        cut_ok += pr.ok() ? 0 : 1;
+    }
+    CHECK(cut_ok == static_cast<int>(whole.size()));
+    for (uint64_t big : {uint64_t{1} << 31, uint64_t{1} << 63, ~uint64_t{0}}) {
+        std::vector<uint8_t> w = whole;
+        for (int k = 0; k < 8; ++k) w[static_cast<size_t>(k)] = static_cast<uint8_t>(big >> (8 * k));
+        packer pr(w);
+        std::string m;
+        pr >> m;
+        CHECK(!pr.ok() && m.empty());
+    }
 }
 
 // ---- server ------------------------------------------------------------------

@@ -441,7 +441,8 @@ def _random_string_batch(kinds, n, rng, maxlen):
 @pytest.mark.parametrize("schema,maxlen,envelope", [
     ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
     ("nested", 64, "response"), ("wide", 24, "request")])
-def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
+@pytest.mark.parametrize("vk", [None, 0, 2], ids=["default", "walk", "tiles"])
+def test_strings_random_vs_oracle(n, schema, maxlen, envelope, vk):
     kinds = {"s": [oracle.STRING],
              "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
              "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
@@ -459,6 +460,8 @@ def test_strings_random_vs_oracle(n, schema, maxlen, envelope):
         p = GpuPacker.for_response(sch, 2)
     else:
         p = GpuPacker(sch)
+    if vk is not None:
+        p.tune(var_kernel=vk)
     want = oracle.pack(kinds, cols, n, p.prefix, list(offs))
     wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
     assert st[0] == 0
@@ -574,12 +577,15 @@ def _check_single_string(kinds, back, boffs, wire, n, rec, prefix):
     assert back[f].tobytes() == mc
 
 
-def test_strings_errors():
+@pytest.mark.parametrize("vk", [None, 0, 2], ids=["default", "walk", "tiles"])
+def test_strings_errors(vk):
     kinds = [oracle.INT32, oracle.STRING]
     n = 1000
     rng = np.random.default_rng(5)
     cols, offs = _random_string_batch(kinds, n, rng, 30)
     p = GpuPacker.for_request(Schema("E", (("x", oracle.INT32), ("s", oracle.STRING))), "Svc::m")
+    if vk is not None:
+        p.tune(var_kernel=vk)
     wire = bytearray(oracle.pack(kinds, cols, n, p.prefix, list(offs)))
     rec = _rec_offsets(kinds, offs, n, len(p.prefix))
     # a length field pointing past its record
@@ -624,7 +630,8 @@ def test_strings_errors():
     assert set(got[small:]) <= {0xA5}
 
 
-def test_strings_empty_frames_then_short_records():
+@pytest.mark.parametrize("vk", [None, 2], ids=["default", "tiles"])
+def test_strings_empty_frames_then_short_records(vk):
     """A block of zero-size records (empty frames: rec[i] == rec[i + 1]) in
     front of short valid records.  Every later record's fast-path output
     offset start - rec[0] - r * fixed_bytes would wrap below zero; the walk
@@ -635,6 +642,8 @@ def test_strings_empty_frames_then_short_records():
     rng = np.random.default_rng(23)
     cols, offs = _random_string_batch(kinds, m, rng, 4)
     p = GpuPacker.for_request(Schema("E", (("x", oracle.INT32), ("s", oracle.STRING))), "Svc::m")
+    if vk is not None:
+        p.tune(var_kernel=vk)
     wire = bytes(oracle.pack(kinds, cols, m, p.prefix, list(offs)))
     rec = _rec_offsets(kinds, offs, m, len(p.prefix))
     for lead in (np.zeros(k, np.uint64), np.full(k, rec[m], np.uint64)):
@@ -702,8 +711,9 @@ def _model_multi_string(kinds, wire: bytes, n, rec, prefix: bytes):
     return (flags, first if first is not None else 2**64 - 1), vals, offs, {f: bytes(c) for f, c in chars.items()}
 
 
+@pytest.mark.parametrize("vk", [None, 2], ids=["default", "tiles"])
 @pytest.mark.parametrize("maxlen", [30, 200])
-def test_multi_strings_errors(maxlen):
+def test_multi_strings_errors(maxlen, vk):
     """Corrupt inputs through the multi-string unpack (the staged walk for
     short records, the global walk for long ones and for records outside a
     non-monotonic index) against the model of the general semantics."""
@@ -713,6 +723,8 @@ def test_multi_strings_errors(maxlen):
     cols, offs = _random_string_batch(kinds, n, rng, maxlen)
     sch = Schema("M", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
     p = GpuPacker.for_request(sch, "Svc::multi")
+    if vk is not None:
+        p.tune(var_kernel=vk)
     clean = bytes(oracle.pack(kinds, cols, n, p.prefix, list(offs)))
     rec = _rec_offsets(kinds, offs, n, len(p.prefix))
 
