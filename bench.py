@@ -53,6 +53,9 @@ def parse():
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--tune", default=None,
                     help="DWORD-path variant rpl,iter,nt (default: the library's tuned default)")
+    ap.add_argument("--strong-records", type=int, default=1 << 26,
+                    help="strong-scaling line beside the weak one: this many records in all, "
+                         "split over the ranks (configs[3]: 64M); 0 disables")
     return ap.parse_args()
 
 
@@ -178,7 +181,16 @@ def main() -> None:
 
     import srpc_amd
     from srpc_amd import QUAD, GpuPacker, _lib
-    from srpc_amd.shard import gather_packed
+    from srpc_amd.shard import NativeComm, gather_packed, shard_range
+
+    # the exchange step: the library's own RCCL gather (srpc_gather_wire) on a
+    # communicator it owns; the id travels over torch's process group
+    comm, comm_note = None, None
+    if world > 1 and args.dist_backend == "nccl":
+        try:
+            comm = NativeComm.from_process_group(local)
+        except Exception as e:  # keep the measurement; say which gather ran
+            comm_note = f"libsrpc_gpu RCCL comm failed ({e}); torch.distributed gather used"
 
     n = args.records
     first = rank * n  # the global batch is one splitmix stream sharded contiguously
@@ -206,7 +218,7 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         ok = all(torch.equal(a, b) for a, b in zip(cols, back))
         verify["roundtrip"] = bool(ok)
-        full = gather_packed(wire, REC_BYTES, n * world) if world > 1 else wire
+        full = gather_packed(wire, REC_BYTES, n * world, comm=comm) if world > 1 else wire
         if rank == 0:
             digest = hashlib.sha256(full.cpu().numpy().tobytes()).hexdigest()
             with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
@@ -294,21 +306,75 @@ def main() -> None:
     gather = None
     if world > 1:
         for _ in range(2):
-            gather_packed(wire, REC_BYTES, n * world)
+            gather_packed(wire, REC_BYTES, n * world, comm=comm)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            gather_packed(wire, REC_BYTES, n * world)
+            gather_packed(wire, REC_BYTES, n * world, comm=comm)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g_ms = (time.perf_counter() - g0) * 1e3 / reps
         moved = n * (world - 1) * REC_BYTES
         gather = {"ms": round(g_ms, 3), "bytes_to_root": moved,
                   "root_ingress_GBps": round(moved / g_ms / 1e6, 1),
-                  "collective": "RCCL gather (ncclSend/ncclRecv to rank 0)" if args.dist_backend == "nccl"
-                  else "gloo gather through host memory (rehearsal only)"}
+                  "collective": ("libsrpc_gpu srpc_gather_wire: RCCL ncclSend/ncclRecv to rank 0 in one group"
+                                 if comm is not None else
+                                 "torch.distributed RCCL gather" if args.dist_backend == "nccl"
+                                 else "gloo gather through host memory (rehearsal only)")}
+        if comm_note:
+            gather["note"] = comm_note
+
+    # Strong scaling (configs[3]): args.strong_records in all, split over the
+    # ranks with the library's shard rule; same step, same clock, max over ranks
+    strong = None
+    if args.strong_records > 0:
+        NS = args.strong_records
+        lo, hi = shard_range(NS, rank, world)
+        m = hi - lo
+        scols = [torch.empty(max(m, 1), dtype=torch.int32, device=dev) for _ in range(4)]
+        sback = [torch.empty(max(m, 1), dtype=torch.int32, device=dev) for _ in range(4)]
+        swire = torch.empty(max(m, 1) * REC_BYTES, dtype=torch.uint8, device=dev)
+        srpc_amd.fill_splitmix_i32(scols, m, 0x5EED, lo, stream)
+
+        def sstep():
+            p.pack(scols, m, swire, stream=stream)
+            p.unpack(swire, m * REC_BYTES, m, sback, stream=stream)
+
+        for _ in range(args.warmup):
+            sstep()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        step0.record(stream)
+        for _ in range(K):
+            sstep()
+        step1.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ts = torch.tensor([max(time.perf_counter() - t0, step0.elapsed_time(step1) / 1e3)], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        st_max = ts.item()
+        sok = all(torch.equal(a[:m], b[:m]) for a, b in zip(scols, sback))
+        full = gather_packed(swire[:m * REC_BYTES], REC_BYTES, NS, comm=comm) if world > 1 else swire[:m * REC_BYTES]
+        sdig = None
+        if rank == 0:
+            sdig = hashlib.sha256(full.cpu().numpy().tobytes()).hexdigest()
+        del full
+        strong = {"records_total": NS, "records_per_gpu_max": max(h - l for l, h in
+                                                                  (shard_range(NS, r, world) for r in range(world))),
+                  "value": round(NS * K * REC_BYTES / 2**30 / st_max, 3), "unit": "GiB/s",
+                  "ms_per_step": round(st_max * 1e3 / K, 4),
+                  "mrecords_per_s": round(NS * K / st_max / 1e6, 1), "roundtrip_rank": bool(sok),
+                  "sha256": sdig, "scaling": "strong"}
+        del scols, sback, swire
 
     # PCIe-inclusive round trip (host columns -> device -> wire -> host), rank 0 only
     pcie = None
@@ -382,6 +448,13 @@ def main() -> None:
         }
         if gather:
             line["gather"] = gather
+        if strong:
+            with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
+                streams = json.load(f)["streams"]
+            want = {st["records"]: st["sha256"] for k, st in streams.items()
+                    if k.startswith("quad_body_")}.get(strong["records_total"])
+            strong["matches_reference"] = (strong["sha256"] == want) if want else None
+            line["strong_scaling"] = strong
         if pcie:
             line["pcie_inclusive"] = pcie
         if world == 1 and args.cpu_seconds > 0:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 1
+#define SRPC_GPU_ABI_VERSION 2
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -190,6 +190,54 @@ int srpc_gpu_unpack_var(const srpc_plan* plan, const uint8_t* d_wire, uint64_t w
                         uint64_t n, const uint64_t* d_rec_offs, void* const* d_cols,
                         uint64_t* const* d_str_offs, srpc_unpack_status* d_status,
                         void* d_scratch, uint64_t scratch_bytes, void* stream);
+
+/* ---- multi-GPU: sharded batches, packed bytes gathered over RCCL -------------
+ * The reference packer appends (core.hpp:34, packer.hpp:73), so a batch
+ * split into contiguous record shards [lo_g, hi_g) in rank order, each packed
+ * on its own GPU, concatenates back to the single-GPU wire exactly.  The only
+ * collective is a gather of the shards' wire bytes to a root (ncclSend /
+ * ncclRecv in one group), bound by the root's xGMI ingress. */
+#define SRPC_SHARD_ALIGN_RECORDS 16  /* shard starts are multiples of 16 records */
+#define SRPC_COMM_ID_BYTES 128       /* an RCCL unique id                         */
+typedef struct srpc_comm srpc_comm;
+
+/* Records [*lo, *hi) of shard `rank` of n records over nranks shards:
+ * contiguous, in rank order, starts aligned to SRPC_SHARD_ALIGN_RECORDS.
+ * Host arithmetic only. */
+int srpc_shard_range(uint64_t n, int rank, int nranks, uint64_t* lo, uint64_t* hi);
+
+/* One process per GPU: rank 0 makes an id, the caller distributes it
+ * (e.g. over its own process group), every rank joins with its device. */
+int srpc_comm_unique_id(uint8_t* id_out /* SRPC_COMM_ID_BYTES */);
+int srpc_comm_init_rank(const uint8_t* id, int nranks, int rank, int device, srpc_comm** out);
+/* One process driving ndev devices: out[g] is rank g on devices[g]. */
+int srpc_comm_init_all(const int* devices, int ndev, srpc_comm** out /* ndev */);
+int srpc_comm_destroy(srpc_comm* comm);
+int srpc_comm_rank(const srpc_comm* comm, int* rank, int* nranks);
+
+/* Each rank contributes one u64 (e.g. its shard's wire bytes, read from the
+ * last entry of its d_rec_offs for string schemas); d_out gets nranks. */
+int srpc_allgather_u64(srpc_comm* comm, const uint64_t* d_in, uint64_t* d_out, void* stream);
+
+/* Gather: every rank calls it with its shard's wire bytes; the root receives
+ * shard r at byte offset sum(h_all_bytes[0..r)) of d_root_wire (root_cap
+ * bytes) -- the single-GPU wire of the whole batch.  h_all_bytes (host, one
+ * entry per rank) is needed on the root only.  Stream-ordered. */
+int srpc_gather_wire(srpc_comm* comm, const uint8_t* d_shard, uint64_t shard_bytes,
+                     uint8_t* d_root_wire, uint64_t root_cap, const uint64_t* h_all_bytes,
+                     int root, void* stream);
+/* The same from one process for all ndev ranks of srpc_comm_init_all
+ * (streams[g] on device g). */
+int srpc_group_gather_wire(srpc_comm* const* comms, int ndev, const uint8_t* const* d_shards,
+                           const uint64_t* h_bytes, uint8_t* d_root_wire, uint64_t root_cap,
+                           int root, void* const* streams);
+/* One process, ndev devices, a fixed-size schema: plans[g] (created on device
+ * g) packs shard g -- d_cols[g] holds records srpc_shard_range(n, g, ndev) on
+ * device g -- into d_shard_wire[g], then the shards are gathered into
+ * d_root_wire on the root. */
+int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comms, int ndev,
+                           const void* const* const* d_cols, uint64_t n, uint8_t* const* d_shard_wire,
+                           uint8_t* d_root_wire, uint64_t root_cap, int root, void* const* streams);
 
 /* ---- utilities --------------------------------------------------------------*/
 

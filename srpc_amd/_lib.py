@@ -25,6 +25,8 @@ SRPC_ERR_BOUNDS = 2
 
 SRPC_STATUS_PREFIX = 1
 SRPC_STATUS_BOUNDS = 2
+SRPC_STATUS_STALLED = 4
+SRPC_COMM_ID_BYTES = 128
 
 SRPC_PATH_DWORD = 1
 SRPC_PATH_TILE = 2
@@ -45,6 +47,16 @@ SIGNATURES = {
     "srpc_gpu_unpack_var": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_fill_splitmix_i32": (C.c_int, [_vp, C.c_uint32, _u64, _u64, _u64, _vp]),
     "srpc_time_next_call": (C.c_int, [_vp, _vp]),
+    "srpc_shard_range": (C.c_int, [_u64, C.c_int, C.c_int, C.POINTER(_u64), C.POINTER(_u64)]),
+    "srpc_comm_unique_id": (C.c_int, [_vp]),
+    "srpc_comm_init_rank": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "srpc_comm_init_all": (C.c_int, [_vp, C.c_int, _vp]),
+    "srpc_comm_destroy": (C.c_int, [_vp]),
+    "srpc_comm_rank": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "srpc_allgather_u64": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "srpc_gather_wire": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, C.c_int, _vp]),
+    "srpc_group_gather_wire": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _u64, C.c_int, _vp]),
+    "srpc_group_pack_gather": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _u64, C.c_int, _vp]),
     "srpc_status_string": (C.c_char_p, [C.c_int]),
     "srpc_gpu_abi_version": (C.c_int, []),
 }

@@ -50,7 +50,8 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, sr
     tmp = target + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-command-line-argument",
-           "-I", os.path.join(ROOT, "include"), "-I", inc] + [f"-D{d}" for d in defines] + ["-o", tmp] + src
+           "-I", os.path.join(ROOT, "include"), "-I", inc] + [f"-D{d}" for d in defines] + ["-o", tmp] + src + [
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     out = subprocess.run(cmd, capture_output=True, text=True)

@@ -26,7 +26,7 @@ def shard_ranges(n: int, world: int, align: int = ALIGN_RECORDS) -> list[tuple[i
     return [shard_range(n, r, world, align) for r in range(world)]
 
 
-def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None):
+def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None, comm: "NativeComm | None" = None):
     """Gather every rank's packed shard into one wire buffer on ``root``.
 
     ``local``: this rank's packed bytes (uint8 tensor on its device, exactly
@@ -51,6 +51,8 @@ def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None):
         raise ValueError(f"rank {rank}: local shard has {local.numel()} bytes, expected {sizes[rank]}")
     if world == 1:
         return local
+    if comm is not None:  # the library's RCCL gather (production path)
+        return comm.gather_wire(local, sizes, root)
     out = None
     if rank == root:
         out = torch.empty(n * record_bytes, dtype=torch.uint8, device=local.device)
@@ -72,3 +74,79 @@ def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None):
         for w in dist.batch_isend_irecv(ops):
             w.wait()
     return out
+
+
+class NativeComm:
+    """One rank of an RCCL communicator owned by libsrpc_gpu (srpc_comm_init_rank):
+    the gather of packed shards runs in the library (ncclSend / ncclRecv to
+    the root inside one group, include/srpc_gpu.h srpc_gather_wire), not
+    through torch.  The 128-byte RCCL id is made by rank 0 and handed to the
+    other ranks over the caller's own process group."""
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+        import ctypes as C
+
+        from . import _lib
+        self.rank, self.nranks, self.device = rank, nranks, device
+        buf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _lib.check(_lib.lib().srpc_comm_init_rank(buf, nranks, rank, device, C.byref(h)), "srpc_comm_init_rank")
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        from . import _lib
+        buf = (C.c_uint8 * _lib.SRPC_COMM_ID_BYTES)()
+        _lib.check(_lib.lib().srpc_comm_unique_id(buf), "srpc_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, device: int, group=None) -> "NativeComm":
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(obj[0], world, rank, device)
+
+    def gather_wire(self, local, all_bytes, root: int = 0, out=None, stream=None):
+        """Every rank: its packed shard (uint8 device tensor).  Root: returns the
+        concatenation in rank order (``out`` or a new tensor); others None."""
+        import ctypes as C
+
+        import torch
+
+        from . import _lib
+        from .packer import _dptr, _stream
+        total = int(sum(all_bytes))
+        if self.rank == root and out is None:
+            out = torch.empty(max(total, 1), dtype=torch.uint8, device=local.device)
+        sizes = (C.c_uint64 * len(all_bytes))(*[int(b) for b in all_bytes])
+        _lib.check(_lib.lib().srpc_gather_wire(self._h, _dptr(local), int(all_bytes[self.rank]),
+                                               _dptr(out) if self.rank == root else None,
+                                               total if self.rank == root else 0, sizes, root,
+                                               _stream(stream)), "srpc_gather_wire")
+        return out[:total] if self.rank == root else None
+
+    def close(self) -> None:
+        from . import _lib
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().srpc_comm_destroy(self._h)
+            self._h.value = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def native_shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """srpc_shard_range of the C ABI (host arithmetic, the same rule as shard_range)."""
+    import ctypes as C
+
+    from . import _lib
+    lo, hi = C.c_uint64(), C.c_uint64()
+    _lib.check(_lib.lib().srpc_shard_range(n, rank, world, C.byref(lo), C.byref(hi)), "srpc_shard_range")
+    return lo.value, hi.value

@@ -37,7 +37,7 @@ def test_library_exports_every_symbol():
 
 def test_library_loads_and_answers_host_calls():
     L = _lib.lib()
-    assert L.srpc_gpu_abi_version() == 1
+    assert L.srpc_gpu_abi_version() == 2
     assert L.srpc_status_string(-2) == b"device pointer misaligned"
     assert L.srpc_status_string(2).startswith(b"wire shorter")
     # argument validation needs no device
@@ -80,3 +80,31 @@ def test_shard_ranges_cover(n, world):
     for lo, _ in rs:
         assert lo % 16 == 0 or lo == n
     assert shard_range(n, 0, 1) == (0, n)
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 1000, 4099, 1 << 24, (1 << 26) + 5, 2**63 + 11])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8])
+def test_native_shard_range_matches_python_rule(n, world):
+    """srpc_shard_range (C ABI, host arithmetic) == srpc_amd.shard.shard_range:
+    contiguous, rank-ordered, every start a multiple of 16 records, so a
+    shard's wire offset is lo * record_bytes and every shard is 16-byte aligned
+    for 1-byte records (the alignment the TILE/DWORD kernels need)."""
+    from srpc_amd.shard import native_shard_range
+    got = [native_shard_range(n, r, world) for r in range(world)]
+    assert got == shard_ranges(n, world)
+    for lo, hi in got:
+        assert lo % 16 == 0 or lo == n
+    # byte offsets of a fixed record size reproduce the single-batch layout
+    rb = 53
+    offs = [lo * rb for lo, _ in got]
+    assert offs[0] == 0 and all(o2 - o1 == (hi - lo) * rb for (lo, hi), o1, o2 in zip(got, offs, offs[1:] + [n * rb]))
+
+
+def test_native_shard_range_rejects_bad_ranks():
+    L = _lib.lib()
+    lo, hi = C.c_uint64(), C.c_uint64()
+    assert L.srpc_shard_range(10, 2, 2, C.byref(lo), C.byref(hi)) == _lib.SRPC_E_INVALID
+    assert L.srpc_shard_range(10, -1, 2, C.byref(lo), C.byref(hi)) == _lib.SRPC_E_INVALID
+    assert L.srpc_shard_range(10, 0, 0, C.byref(lo), C.byref(hi)) == _lib.SRPC_E_INVALID
+    assert L.srpc_comm_destroy(None) == _lib.SRPC_E_INVALID
+    assert L.srpc_gather_wire(None, None, 0, None, 0, None, 0, None) == _lib.SRPC_E_INVALID
