@@ -82,7 +82,8 @@ typedef enum srpc_kind {
  * Reset by the call itself (stream-ordered) before decoding starts. */
 typedef struct srpc_unpack_status {
     uint32_t flags;             /* OR of SRPC_STATUS_* over the batch          */
-    uint32_t reserved;
+    uint32_t reserved;          /* diagnostics: bit 0 = srpc_gpu_unpack_var_stream
+                                   walked a mis-speculated chunk again        */
     uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */
 } srpc_unpack_status;
 
@@ -190,6 +191,26 @@ int srpc_gpu_unpack_var(const srpc_plan* plan, const uint8_t* d_wire, uint64_t w
                         uint64_t n, const uint64_t* d_rec_offs, void* const* d_cols,
                         uint64_t* const* d_str_offs, srpc_unpack_status* d_status,
                         void* d_scratch, uint64_t scratch_bytes, void* stream);
+
+/* Unpack n records from a stream with NO record index -- the reference's own
+ * decode of a concatenated batch with one shared cursor (buffer::_offset,
+ * core.hpp:39; packer.hpp:210-222) -- e.g. the bytes a reference packer
+ * appended.  The record starts are found on the device (speculative walks of
+ * 512-byte chunks from plausible record starts, each checked against its
+ * predecessor's exit, wrong ones walked again in order) and written to
+ * d_rec_offs[0..n]; then the records are decoded as by srpc_gpu_unpack_var.
+ * The first record the cursor cannot read (prefix mismatch, or a field /
+ * string past the end) is reported in *d_status as the first bad record
+ * (PREFIX or BOUNDS), as orc_unpack / the reference would meet it; its start
+ * is d_rec_offs[i] and every later entry is wire_len (those records are
+ * BOUNDS too).  Scratch: srpc_plan_var_stream_scratch_bytes (256-byte
+ * aligned). */
+int srpc_plan_var_stream_scratch_bytes(const srpc_plan* plan, uint64_t n, uint64_t wire_len,
+                                       uint64_t* out);
+int srpc_gpu_unpack_var_stream(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len,
+                               uint64_t n, uint64_t* d_rec_offs, void* const* d_cols,
+                               uint64_t* const* d_str_offs, srpc_unpack_status* d_status,
+                               void* d_scratch, uint64_t scratch_bytes, void* stream);
 
 /* ---- multi-GPU: sharded batches, packed bytes gathered over RCCL -------------
  * The reference packer appends (core.hpp:34, packer.hpp:73), so a batch

@@ -1,0 +1,461 @@
+// stream.hip -- decode a concatenated record stream with no index
+// (srpc_gpu_unpack_var_stream).
+//
+// The reference decodes a batch with ONE shared cursor (buffer::_offset,
+// core.hpp:39): each pipe_output advances it (packer.hpp:210-222, nested
+// unpack sharing the buffer as in tests/packer_test.cpp:77-88), so where a
+// record starts is only known once every record before it was read.  Here
+// the record index is found on the device, then the indexed decode runs.
+//
+// 1. k_stream_spec -- the wire is cut into chunks of kChunk bytes, one lane
+//    each.  A lane takes the first position p of its chunk at which kPlaus
+//    records parse one after another (a plausible record start: a string
+//    length read at a wrong offset is almost always past the end of the
+//    wire) and walks records from there while they start inside the chunk:
+//    record count, the position after them ("exit": the first record start
+//    at or past the chunk end, or where a record failed to parse), and why
+//    the walk stopped.
+// 2. k_stream_check -- chunk c is right when its start equals the exit of
+//    chunk c - 1 (or chunk c holds no record start at all), chunk 0 when it
+//    starts at 0.  By induction every chunk up to the first wrong one is
+//    right.
+// 3. k_stream_fix (one workgroup, runs only if a chunk was wrong) -- walks the
+//    chunks from the first wrong one in order, each from its predecessor's
+//    corrected exit, until the stream stops; chunks whose start already
+//    agrees are taken as they are.
+// 4. the chunks' record counts are scanned to record numbers, and
+//    k_stream_index writes rec_offs[] by walking each chunk again;
+//    k_stream_tail fills what the stream does not hold.
+// The walk is orc_unpack's cursor (oracle/packer_oracle.c): the prefix must
+// match, every read must fit in the wire.  A record that fails stops the
+// stream: its start becomes rec_offs[i], every later entry wire_len, so the
+// indexed decode reports it (PREFIX or BOUNDS) as the first bad record, and
+// every later record as BOUNDS.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+
+#include "plan.h"
+#include "srpc_gpu.h"
+
+namespace srpc_impl {
+namespace {
+
+constexpr uint32_t kChunk = 512;    // wire bytes per speculating lane
+constexpr int kPlaus = 3;           // records that must parse from a candidate start
+constexpr uint64_t kNone = ~0ull;   // chunk holds no plausible record start
+constexpr uint32_t kStopEnd = 1;    // the walk reached the end of the wire exactly
+constexpr uint32_t kStopBad = 2;    // a record failed to parse at the exit position
+
+struct StreamArgs {
+    uint32_t size[kMaxFields];  // fixed field bytes, 0 = string
+    const uint8_t* prefix;      // device copy (16 zero bytes past the end)
+    uint32_t nfields, prefix_len;
+};
+
+struct Chunks {      // per chunk (scratch, C entries each)
+    uint64_t* start;  // first record start walked from (kNone: none in the chunk)
+    uint64_t* cnt;    // records starting in [start, chunk end)
+    uint64_t* exit;   // position after them
+    uint32_t* stop;   // kStopEnd / kStopBad / 0
+    uint32_t* bad;    // chunk disagrees with its predecessor
+    uint32_t* blk;    // per 256 chunks: bit 0 some chunk is bad, bit 1 some chunk stops
+    uint32_t* ctl;    // [0] any bad, [1] the stream's stop chunk, [2] the first bad chunk
+};
+
+template <typename T>
+__device__ __forceinline__ T ld(const uint8_t* p) {
+    T v;
+    __builtin_memcpy(&v, p, sizeof(T));
+    return v;
+}
+
+// orc_unpack's cursor over one record at p: the position after it, or p with
+// *err set (SRPC_STATUS_PREFIX / SRPC_STATUS_BOUNDS).
+__device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint32_t* err) {
+    *err = 0;
+    if (a.prefix_len) {
+        if (a.prefix_len > W - p) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        uint32_t i = 0;
+        for (; i + 8 <= a.prefix_len; i += 8)
+            if (ld<uint64_t>(w + p + i) != ld<uint64_t>(a.prefix + i)) {
+                *err = SRPC_STATUS_PREFIX;
+                return p;
+            }
+        for (; i < a.prefix_len; ++i)
+            if (w[p + i] != a.prefix[i]) {
+                *err = SRPC_STATUS_PREFIX;
+                return p;
+            }
+    }
+    uint64_t q = p + a.prefix_len;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            if (sz > W - q) {
+                *err = SRPC_STATUS_BOUNDS;
+                return p;
+            }
+            q += sz;
+            continue;
+        }
+        if (8 > W - q) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        const uint64_t len = ld<uint64_t>(w + q);
+        q += 8;
+        if (len > W - q) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        q += len;
+    }
+    return q;
+}
+
+// Walk from p while records start before hi: count, exit, stop reason.
+__device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint64_t hi, uint64_t* cnt,
+                     uint64_t* exit, uint32_t* stop) {
+    uint64_t k = 0;
+    *stop = 0;
+    while (p < hi) {
+        uint32_t err;
+        const uint64_t q = parse_at(a, w, W, p, &err);
+        if (err) {
+            *stop = kStopBad;
+            break;
+        }
+        ++k;
+        p = q;
+    }
+    if (!*stop && p >= W) *stop = kStopEnd;
+    *cnt = k;
+    *exit = p;
+}
+
+__device__ __forceinline__ bool plausible(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p) {
+    for (int k = 0; k < kPlaus; ++k) {
+        if (p == W) return k > 0;  // the stream may end right after a record
+        uint32_t err;
+        const uint64_t q = parse_at(a, w, W, p, &err);
+        if (err) return false;
+        p = q;
+    }
+    return true;
+}
+
+// Chunk c's speculation: its first plausible record start, the records from
+// there that start inside the chunk, and the position after them.  A chunk
+// with no plausible start (inside a long record) passes its entry through:
+// start = exit = kNone, no records.
+__global__ __launch_bounds__(kBlock) void k_stream_spec(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+                                                        uint64_t C, Chunks ch) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t lo = c * kChunk, hi = min(lo + kChunk, W);
+    uint64_t b = kNone;
+    if (c == 0) {
+        b = 0;  // the stream starts at 0: no speculation
+    } else {
+        for (uint64_t p = lo; p < hi; ++p)
+            if (plausible(a, w, W, p)) {
+                b = p;
+                break;
+            }
+    }
+    uint64_t cnt = 0, exit = kNone;
+    uint32_t stop = 0;
+    if (b != kNone) walk(a, w, W, b, hi, &cnt, &exit, &stop);
+    ch.start[c] = b;
+    ch.cnt[c] = cnt;
+    ch.exit[c] = exit;
+    ch.stop[c] = stop;
+    if (stop) atomicOr(&ch.blk[c >> 8], 2u);
+}
+
+// The entry of chunk c (the first record start at or after its beginning):
+// the exit of the nearest chunk before it with a record start, or a stop.
+__device__ __forceinline__ uint64_t entry_of(const Chunks& ch, uint64_t c, bool* stopped) {
+    *stopped = false;
+    for (uint64_t j = c; j-- > 0;) {
+        if (ch.start[j] == kNone) continue;  // passes its own entry through
+        *stopped = ch.stop[j] != 0;
+        return ch.exit[j];
+    }
+    return 0;  // unreachable: chunk 0 always starts at 0
+}
+
+// Chunk c agrees with its entry e when it starts exactly there, or -- e past
+// the chunk's end -- when it found no record start.
+__device__ __forceinline__ bool agrees(uint64_t e, uint64_t chunk_hi, uint64_t start) {
+    return e >= chunk_hi ? start == kNone : start == e;
+}
+
+__global__ __launch_bounds__(kBlock) void k_stream_check(uint64_t W, uint64_t C, Chunks ch) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C || c == 0) {
+        if (c == 0 && c < C) ch.bad[0] = 0;
+        return;
+    }
+    const uint64_t hi = min((c + 1) * kChunk, W);
+    bool stopped;
+    const uint64_t e = entry_of(ch, c, &stopped);
+    // after a stop nothing counts (masked later); otherwise start must agree
+    const bool ok = stopped || agrees(e, hi, ch.start[c]);
+    ch.bad[c] = ok ? 0u : 1u;
+    if (!ok) {
+        atomicOr(&ch.blk[c >> 8], 1u);
+        atomicOr(&ch.ctl[0], 1u);
+        atomicMin(&ch.ctl[2], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
+    }
+}
+
+// The stream's stop among the chunks before the first bad one (all right).
+__global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c < C && c < ch.ctl[2] && ch.stop[c] && ch.start[c] != kNone)
+        atomicMin(&ch.ctl[1], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
+}
+
+// One workgroup, thread 0, only when some chunk before the stream's stop is
+// bad: from the first bad chunk on, every chunk in order from its
+// predecessor's (corrected) exit until the stream stops.  Chunks that agree
+// are kept; 256-chunk blocks with no bad chunk and no stop are skipped.
+__global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W, uint64_t C, Chunks ch) {
+    if (threadIdx.x != 0 || ch.ctl[0] == 0 || ch.ctl[1] < ch.ctl[2]) return;
+    uint64_t c = ch.ctl[2];
+    while (c < C) {
+        const uint64_t hi = min((c + 1) * kChunk, W);
+        bool stopped;
+        const uint64_t e = entry_of(ch, c, &stopped);
+        if (stopped) {  // the stream stopped before chunk c (in a chunk already right)
+            return;
+        }
+        const bool fix = ch.bad[c] || !agrees(e, hi, ch.start[c]);
+        if (fix) {
+            uint64_t cnt = 0, exit = kNone, start = kNone;
+            uint32_t stop = 0;
+            if (e < hi) {
+                start = e;
+                walk(a, w, W, e, hi, &cnt, &exit, &stop);
+            }
+            ch.start[c] = start;
+            ch.cnt[c] = cnt;
+            ch.exit[c] = exit;
+            ch.stop[c] = stop;
+            ch.bad[c] = 0;
+        }
+        if (ch.stop[c] && ch.start[c] != kNone) {
+            ch.ctl[1] = static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull));
+            return;
+        }
+        ++c;
+        // skip blocks that hold neither a bad chunk nor a stop: they agree --
+        // unless this chunk was just corrected (the next block's first chunk
+        // was checked against its old exit)
+        while (!fix && c < C && (c & 255) == 0 && ch.blk[c >> 8] == 0) c += 256;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_stream_mask(uint64_t C, Chunks ch, uint64_t* counts) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c < C) counts[c] = c > ch.ctl[1] ? 0 : ch.cnt[c];
+}
+
+// rec_offs[recbase[c] + k] for the chunk's records (k-th start), up to index n.
+__global__ __launch_bounds__(kBlock) void k_stream_index(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+                                                         uint64_t C, Chunks ch, const uint64_t* __restrict__ counts,
+                                                         const uint64_t* __restrict__ recbase, uint64_t n,
+                                                         uint64_t* __restrict__ rec_offs) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C || counts[c] == 0) return;
+    uint64_t r = recbase[c];
+    if (r > n) return;
+    uint64_t p = ch.start[c];
+    for (uint64_t k = 0; k < counts[c] && r <= n; ++k, ++r) {  // [n]: the start of record n, if any
+        rec_offs[r] = p;
+        uint32_t err;
+        p = parse_at(a, w, W, p, &err);
+    }
+}
+
+// Records the stream holds: T = sum of counts.  rec_offs[T] = where the stream
+// stopped (the failing record's start, or the end of the last record);
+// rec_offs[T + 1 .. n] = W.  With T >= n, rec_offs[n] = the start of record n
+// (or the end of record n - 1).
+__global__ __launch_bounds__(kBlock) void k_stream_tail(uint64_t W, uint64_t C, Chunks ch,
+                                                        const uint64_t* __restrict__ recbase, uint64_t n,
+                                                        uint64_t* __restrict__ rec_offs) {
+    const uint64_t S = ch.ctl[1];
+    const uint64_t T = recbase[C];  // total (the scan's last entry)
+    const uint64_t end = (C && S < C && ch.start[S] != kNone) ? ch.exit[S] : W;
+    const uint64_t gs = static_cast<uint64_t>(gridDim.x) * kBlock;
+    for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; r <= n; r += gs) {
+        if (r < T) continue;  // written by k_stream_index (r < n)
+        rec_offs[r] = r == T ? end : W;
+    }
+}
+
+// Diagnostic (srpc_unpack_status.reserved bit 0): some speculated chunk had
+// to be walked again.
+__global__ void k_stream_note(const Chunks ch, srpc_unpack_status* st) {
+    if (threadIdx.x == 0 && ch.ctl[0]) atomicOr(&st->reserved, 1u);
+}
+
+__global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ch.ctl[0] = 0;            // some chunk is bad
+        ch.ctl[1] = 0xffffffffu;  // the chunk where the stream stops
+        ch.ctl[2] = 0xffffffffu;  // the first bad chunk
+    }
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nblk;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        ch.blk[i] = 0;
+}
+
+uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
+
+struct StreamLayout {
+    uint64_t C, start, cnt, exit, counts, recbase, stop, bad, blk, ctl, total;
+};
+
+StreamLayout stream_layout(uint64_t wire_len) {
+    StreamLayout L{};
+    L.C = std::max<uint64_t>(1, (wire_len + kChunk - 1) / kChunk);
+    uint64_t o = 0;
+    L.start = o;
+    o += r256(8 * L.C);
+    L.cnt = o;
+    o += r256(8 * L.C);
+    L.exit = o;
+    o += r256(8 * L.C);
+    L.counts = o;
+    o += r256(8 * L.C);
+    L.recbase = o;
+    o += r256(8 * (L.C + 1));
+    L.stop = o;
+    o += r256(4 * L.C);
+    L.bad = o;
+    o += r256(4 * L.C);
+    L.blk = o;
+    o += r256(4 * ((L.C + 255) / 256));
+    L.ctl = o;
+    o += 256;
+    L.total = o;
+    return L;
+}
+
+// Device scan of counts[0..C) into recbase[0..C] (exclusive, [C] = total),
+// one workgroup per 2048 values + a partials pass (C is small: wire / 512).
+__global__ __launch_bounds__(kBlock) void k_small_scan(const uint64_t* __restrict__ v, uint64_t C,
+                                                       uint64_t* __restrict__ out) {
+    // a single workgroup walks the array in 256-value steps with a running total
+    __shared__ uint64_t wsum[kBlock / 64];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t base = 0; base < C; base += kBlock) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t x = i < C ? v[i] : 0;
+        uint64_t inc = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint64_t before = carry, all = 0;
+        for (int k = 0; k < kBlock / 64; ++k) {
+            before += k < wave ? wsum[k] : 0;
+            all += wsum[k];
+        }
+        if (i < C) out[i] = before + inc - x;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[C] = carry;
+}
+
+}  // namespace
+}  // namespace srpc_impl
+
+using namespace srpc_impl;
+
+extern "C" {
+
+int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out) {
+    if (!p || !out || !p->has_string) return SRPC_E_INVALID;
+    uint64_t var = 0;
+    if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
+    *out = r256(var) + stream_layout(wire_len).total;
+    return SRPC_OK;
+}
+
+int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                               uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                               srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (!p || !p->has_string || !rec_offs || !scratch) return SRPC_E_INVALID;
+    if (wire_len && !wire) return SRPC_E_INVALID;
+    if (!aligned(rec_offs, 8) || !aligned(scratch, 256)) return SRPC_E_ALIGN;
+    uint64_t need = 0, var = 0;
+    if (int rc = srpc_plan_var_stream_scratch_bytes(p, n, wire_len, &need)) return rc;
+    if (scratch_bytes < need) return SRPC_E_CAPACITY;
+    srpc_plan_var_scratch_bytes(p, n, wire_len, &var);
+    auto s = static_cast<hipStream_t>(stream);
+    auto* base = static_cast<uint8_t*>(scratch) + r256(var);
+    const StreamLayout L = stream_layout(wire_len);
+    Chunks ch{reinterpret_cast<uint64_t*>(base + L.start), reinterpret_cast<uint64_t*>(base + L.cnt),
+              reinterpret_cast<uint64_t*>(base + L.exit),  reinterpret_cast<uint32_t*>(base + L.stop),
+              reinterpret_cast<uint32_t*>(base + L.bad),   reinterpret_cast<uint32_t*>(base + L.blk),
+              reinterpret_cast<uint32_t*>(base + L.ctl)};
+    auto* counts = reinterpret_cast<uint64_t*>(base + L.counts);
+    auto* recbase = reinterpret_cast<uint64_t*>(base + L.recbase);
+    StreamArgs a{};
+    for (uint32_t f = 0; f < p->nfields; ++f) a.size[f] = p->size[f];
+    a.prefix = p->d_prefix;
+    a.nfields = p->nfields;
+    a.prefix_len = p->prefix_len;
+    const uint64_t C = L.C;
+    const uint64_t g = (C + kBlock - 1) / kBlock;
+    if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    const TimedCall timed;
+    const uint64_t nblk = (C + 255) / 256;
+    launch(k_stream_ctl_reset, dim3(static_cast<uint32_t>(std::min<uint64_t>((nblk + 255) / 256 + 1, 1024))),
+           dim3(256), 0, s, ch, nblk);
+    if (wire_len) {
+        launch(k_stream_spec, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+        launch(k_stream_check, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
+        launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
+        launch(k_stream_fix, dim3(1), dim3(64), 0, s, a, wire, wire_len, C, ch);
+        launch(k_stream_mask, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch, counts);
+    } else {
+        launch(k_stream_mask, dim3(1), dim3(kBlock), 0, s, 0ull, ch, counts);
+    }
+    launch(k_small_scan, dim3(1), dim3(kBlock), 0, s, static_cast<const uint64_t*>(counts), wire_len ? C : 0ull,
+           recbase);
+    if (wire_len)
+        launch(k_stream_index, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch,
+               static_cast<const uint64_t*>(counts), static_cast<const uint64_t*>(recbase), n, rec_offs);
+    launch(k_stream_tail, dim3(static_cast<uint32_t>(std::min<uint64_t>(n / kBlock + 1, 4096))), dim3(kBlock), 0, s,
+           wire_len, wire_len ? C : 0ull, ch, static_cast<const uint64_t*>(recbase), n, rec_offs);
+    if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    // the indexed decode over the index just built (the timing hook, if armed,
+    // covers the index kernels above only)
+    const int rc = srpc_gpu_unpack_var(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch, var, stream);
+    if (rc == SRPC_OK && st) {
+        hipLaunchKernelGGL(k_stream_note, dim3(1), dim3(64), 0, s, ch, st);
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    }
+    return rc;
+}
+
+}  // extern "C"

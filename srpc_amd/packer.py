@@ -204,6 +204,23 @@ class GpuPacker:
                                              _stream(stream)),
               "srpc_gpu_unpack_var")
 
+    def var_stream_scratch_bytes(self, n: int, wire_len: int) -> int:
+        """Device scratch for unpack_var_stream (256-byte aligned)."""
+        out = C.c_uint64()
+        check(_lib.lib().srpc_plan_var_stream_scratch_bytes(self._h, n, wire_len, C.byref(out)),
+              "srpc_plan_var_stream_scratch_bytes")
+        return out.value
+
+    def unpack_var_stream(self, wire, wire_len: int, n: int, rec_offs, cols: Sequence, str_offs: Sequence,
+                          scratch, scratch_bytes: int, status=None, stream=None) -> None:
+        """Unpack n records from a concatenated stream with no index (the
+        reference's shared-cursor decode); writes rec_offs[0..n] (async)."""
+        check(_lib.lib().srpc_gpu_unpack_var_stream(self._h, _dptr(wire), wire_len, n, _dptr(rec_offs),
+                                                    self._cols(cols), self._str_offs(str_offs),
+                                                    _dptr(status), _dptr(scratch), scratch_bytes,
+                                                    _stream(stream)),
+              "srpc_gpu_unpack_var_stream")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.lib().srpc_plan_destroy(self._h)

@@ -1,0 +1,213 @@
+"""Index-free decode of a concatenated string-record stream on the GPU
+(srpc_gpu_unpack_var_stream): the reference's own shared-cursor decode
+(core.hpp:39, packer.hpp:210-222) of the bytes its packer appends, with no
+record index.  Checked against the oracle's cursor (oracle/packer_oracle.c
+orc_unpack) and the reference-produced fixtures:
+- the reference's multiple_strings.bin (301 records, strings 0..300 bytes);
+- the packer_test.cpp vectors repeated 100,003 times;
+- random schemas, short and long strings (chunks inside one record pass
+  their entry on), and zero-heavy data on which the speculative starts are
+  often wrong (the in-order fixer then walks the chunks again);
+- streams cut short, foreign prefixes, fewer records than asked for, and
+  trailing bytes after the n-th record.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import srpc_amd
+from srpc_amd import GpuPacker, Schema
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip("no GPU", allow_module_level=True)
+
+from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty, host, read_status, status_buf  # noqa: E402
+
+GPU_OF_ORC = {oracle.ORC_ERR_BOUNDS: srpc_amd.SRPC_STATUS_BOUNDS, oracle.ORC_ERR_PREFIX: srpc_amd.SRPC_STATUS_PREFIX}
+
+
+def stream_unpack(p, kinds, wire: bytes, n):
+    W = len(wire)
+    w = dev(np.frombuffer(wire, np.uint8)) if W else empty(16)
+    outs, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            outs.append(empty(W + 16))
+            offs.append(empty(8 * (n + 1)))
+        else:
+            outs.append(empty(n * oracle.KIND_SIZE[k] + 16))
+            offs.append(None)
+    sb = p.var_stream_scratch_bytes(n, W)
+    scratch = torch.empty(sb + 256, dtype=torch.uint8, device="cuda:0")
+    base = (-scratch.data_ptr()) % 256
+    rec = empty(8 * (n + 1))
+    st = status_buf()
+    p.unpack_var_stream(w, W, n, rec, outs, offs, scratch.data_ptr() + base, sb, st)
+    rec_h = host(rec, 8 * (n + 1), np.uint64)
+    stream_unpack.last_reserved = int(host(st, 8)[4:8].view(np.uint32)[0])
+    res, res_offs = [], []
+    for k, o, so in zip(kinds, outs, offs):
+        if k == oracle.STRING:
+            oh = host(so, 8 * (n + 1), np.uint64)
+            res_offs.append(oh)
+            res.append(host(o, int(oh[n])) if n else np.zeros(0, np.uint8))
+        else:
+            res_offs.append(None)
+            res.append(host(o, n * oracle.KIND_SIZE[k], oracle.KIND_DTYPE[k]))
+    return res, res_offs, rec_h, read_status(st)
+
+
+def check_clean(p, kinds, wire, n):
+    """A stream of exactly n well-formed records: everything equals the oracle."""
+    back, boffs, rec, st = stream_unpack(p, kinds, wire, n)
+    rc, ocols, ooffs, consumed, _ = oracle.unpack(kinds, wire, n, p.prefix)
+    assert rc == oracle.ORC_OK
+    assert st == (0, 2**64 - 1)
+    for f, k in enumerate(kinds):
+        assert back[f].tobytes() == ocols[f].tobytes(), f
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f], ooffs[f]), f
+    return rec
+
+
+def test_reference_fixture_without_index(golden_dir):
+    z = np.load(os.path.join(golden_dir, "multiple_strings_in.npz"))
+    kinds = [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]
+    p = GpuPacker(Schema("multiple_primitives", tuple((f"a{i}", k) for i, k in enumerate(kinds))))
+    wire = open(os.path.join(golden_dir, "multiple_strings.bin"), "rb").read()
+    n = len(z["a1"])
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, [None, None, None, z["offs"]], n))
+
+
+@pytest.mark.parametrize("reps", [1, 100_003])
+@pytest.mark.parametrize("which", ["unpack request/multiple", "unpack response/nested"])
+def test_packer_test_vectors_repeated(which, reps):
+    with open(os.path.join(os.path.dirname(__file__), "golden", "packer_test_vectors.json")) as f:
+        case = {c["section"]: c for c in json.load(f)}[which]
+    one = bytes.fromhex(case["input"])
+    if "multiple" in which:
+        kinds = [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]
+        p = GpuPacker.for_request(Schema("multiple_primitives", tuple((f"a{i}", k) for i, k in enumerate(kinds))),
+                                  case["method"])
+    else:
+        kinds = [oracle.INT64, oracle.INT8, oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]
+        p = GpuPacker.for_response(Schema("nested_message", tuple((f"a{i}", k) for i, k in enumerate(kinds))),
+                                   case["code"])
+    rec = check_clean(p, kinds, one * reps, reps)
+    assert np.array_equal(rec, np.arange(reps + 1, dtype=np.uint64) * np.uint64(len(one)))
+
+
+KINDS = {"s": [oracle.STRING],
+         "mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
+         "two_str": [oracle.STRING, oracle.INT32, oracle.STRING],
+         "nested": [oracle.INT64, oracle.INT8, oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]}
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 1000, 30_001])
+@pytest.mark.parametrize("schema,maxlen,envelope", [("s", 40, None), ("mixed", 300, None),
+                                                    ("two_str", 16, "request"), ("s", 5000, None),
+                                                    ("nested", 64, "response")])
+def test_random_streams(n, schema, maxlen, envelope):
+    kinds = KINDS[schema]
+    if maxlen > 1000 and n > 3000:
+        n = 3000
+    rng = np.random.default_rng(n * 3 + maxlen)
+    cols, offs = _random_string_batch(kinds, n, rng, maxlen)
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = (GpuPacker.for_request(sch, "Svc_servicer::m") if envelope == "request"
+         else GpuPacker.for_response(sch, 2) if envelope == "response" else GpuPacker(sch))
+    wire = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
+
+
+@pytest.mark.parametrize("n", [257, 20_000])
+def test_zero_heavy_streams_misspeculate_and_fix(n):
+    """Zero bytes everywhere: a string length read at a wrong offset is often
+    0, so many chunks speculate a wrong start; the in-order fixer walks them
+    again.  The result must still be exact."""
+    kinds = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
+    rng = np.random.default_rng(n)
+    cols, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            lens = rng.integers(0, 24, n).astype(np.uint64)
+            lens[rng.random(n) < 0.5] = 0
+            o = np.zeros(n + 1, np.uint64)
+            o[1:] = np.cumsum(lens)
+            c = np.zeros(max(1, int(o[-1])), np.uint8)
+            c[rng.random(c.size) < 0.05] = 7
+            cols.append(c)
+            offs.append(o)
+        else:
+            dt = np.dtype(oracle.KIND_DTYPE[k])
+            cols.append(np.zeros(n, dt))
+            offs.append(None)
+    p = GpuPacker(Schema("Z", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    wire = oracle.pack(kinds, cols, n, b"", list(offs))
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
+    assert stream_unpack.last_reserved & 1, "expected the fixer to run on zero-heavy data"
+
+
+def _error_case(p, kinds, wire, n):
+    """The first record the cursor cannot read is reported as the oracle meets
+    it, and every record before it decodes exactly."""
+    back, boffs, rec, st = stream_unpack(p, kinds, wire, n)
+    rc, ocols, ooffs, consumed, err = oracle.unpack(kinds, wire, n, p.prefix)
+    assert rc != oracle.ORC_OK
+    assert st[1] == err and st[0] & GPU_OF_ORC[rc], (st, rc, err)
+    assert int(rec[err]) == consumed or rc == oracle.ORC_ERR_BOUNDS
+    for f, k in enumerate(kinds):
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f][:err + 1], ooffs[f][:err + 1]), f
+            assert back[f].tobytes()[:int(ooffs[f][err])] == ocols[f].tobytes()[:int(ooffs[f][err])], f
+        else:
+            assert back[f][:err].tobytes() == ocols[f][:err].tobytes(), f
+
+
+def test_stream_errors():
+    kinds = KINDS["mixed"]
+    n = 5000
+    rng = np.random.default_rng(99)
+    cols, offs = _random_string_batch(kinds, n, rng, 60)
+    p = GpuPacker.for_request(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))), "Svc::stream")
+    wire = bytes(oracle.pack(kinds, cols, n, p.prefix, list(offs)))
+    rec = _rec_offsets(kinds, offs, n, len(p.prefix))
+    # cut short at several places (inside a prefix, a length, chars, a fixed field)
+    for cut in (int(rec[1234]) + 3, int(rec[2000]) + len(p.prefix) + 4, int(rec[4999]) + 40, int(rec[n]) - 1):
+        _error_case(p, kinds, wire[:cut], n)
+    # a foreign method name in record 3100
+    bad = bytearray(wire)
+    bad[int(rec[3100]) + 10] ^= 0x04
+    _error_case(p, kinds, bytes(bad), n)
+    # a string length past the end of the wire in record 17
+    bad = bytearray(wire)
+    at = int(rec[17]) + len(p.prefix) + 1
+    bad[at:at + 8] = (2**40).to_bytes(8, "little")
+    _error_case(p, kinds, bytes(bad), n)
+    # more records asked for than the stream holds
+    _error_case(p, kinds, wire, n + 7)
+
+
+def test_trailing_bytes_after_n_records():
+    kinds = KINDS["two_str"]
+    n = 3000
+    rng = np.random.default_rng(4)
+    cols, offs = _random_string_batch(kinds, n, rng, 20)
+    p = GpuPacker(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    wire = oracle.pack(kinds, cols, n, b"", list(offs))
+    m = 2222
+    back, boffs, rec, st = stream_unpack(p, kinds, wire, m)
+    rc, ocols, ooffs, _, _ = oracle.unpack(kinds, wire, m, b"")
+    assert rc == oracle.ORC_OK and st == (0, 2**64 - 1)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n)[:m + 1])
+    for f, k in enumerate(kinds):
+        assert back[f].tobytes() == ocols[f].tobytes(), f
