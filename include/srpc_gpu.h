@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 2
+#define SRPC_GPU_ABI_VERSION 3
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -259,6 +259,40 @@ int srpc_group_gather_wire(srpc_comm* const* comms, int ndev, const uint8_t* con
 int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comms, int ndev,
                            const void* const* const* d_cols, uint64_t n, uint8_t* const* d_shard_wire,
                            uint8_t* d_root_wire, uint64_t root_cap, int root, void* const* streams);
+
+/* ---- framed request batches of several methods (server side) ----------------
+ * The reference server reads one frame (transport.hpp recv_data: BE32 length |
+ * payload) and dispatches it by the method name it starts with (server.hpp:
+ * 58-69).  A batch read from a socket holds frames of any method in any order.
+ * srpc_frames_classify puts frame i (bytes [d_offs[i], d_offs[i+1]) of d_buf,
+ * the last frame ending at buf_len) into bucket k when it is exactly one record
+ * of req_plans[k] -- a fixed-size plan whose prefix is the frame's constant
+ * `BE32 len | str(method) | str(Req::name)`: same length, same prefix; the
+ * first matching plan wins.  Outputs (device):
+ *   d_class[i]             k, or SRPC_FRAME_UNKNOWN (the caller answers it);
+ *   d_index[k*nframes + j] the frames of bucket k (j < d_counts[k]; order
+ *                          within a bucket is unspecified);
+ *   d_counts[0..nplans+1]  frames per bucket, then the response stream's total
+ *                          bytes, then the number of unknown frames;
+ *   d_out_off[0..nframes]  byte offset of frame i's response in the batch's
+ *                          response stream (resp_bytes[k] per frame of bucket
+ *                          k, 0 for unknown frames), total at [nframes].
+ * nplans <= SRPC_FRAMES_MAX_PLANS.  Scratch: srpc_frames_scratch_bytes, 8-byte
+ * aligned.  Stream-ordered; nothing is synchronised. */
+#define SRPC_FRAME_UNKNOWN 0xFF
+#define SRPC_FRAMES_MAX_PLANS 16
+int srpc_frames_scratch_bytes(uint64_t nframes, int nplans, uint64_t* out);
+int srpc_frames_classify(const srpc_plan* const* req_plans, const uint32_t* resp_bytes, int nplans,
+                         const uint8_t* d_buf, uint64_t buf_len, const uint32_t* d_offs,
+                         uint64_t nframes, uint8_t* d_class, uint32_t* d_index, uint64_t* d_counts,
+                         uint64_t* d_out_off, void* d_scratch, uint64_t scratch_bytes, void* stream);
+/* d_out[j*record_bytes ..] = the record_bytes bytes at d_buf + d_offs[d_index[j]], j < n. */
+int srpc_frames_gather(const uint8_t* d_buf, const uint32_t* d_offs, const uint32_t* d_index,
+                       uint64_t n, uint32_t record_bytes, uint8_t* d_out, void* stream);
+/* d_out + d_out_off[d_index[j]] = response j (record_bytes bytes of d_resp), j < n. */
+int srpc_frames_scatter(const uint8_t* d_resp, const uint32_t* d_index, uint64_t n,
+                        uint32_t record_bytes, const uint64_t* d_out_off, uint8_t* d_out,
+                        void* stream);
 
 /* ---- utilities --------------------------------------------------------------*/
 

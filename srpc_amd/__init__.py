@@ -6,7 +6,8 @@ tests and ``bench.py``.  C++ callers use ``include/srpc/gpu.hpp`` instead.
 """
 from .packer import (BOOL, CHAR, INT8, INT16, INT32, INT64, RPC_ERR_FUNCTION_NOT_REGISTERED,
                      RPC_ERR_RECV_TIMEOUT, RPC_SUCCESS, STRING, GpuPacker, Schema, SrpcError,
-                     fill_splitmix_i32, request_prefix, response_prefix, time_next_call)
+                     fill_splitmix_i32, request_prefix, response_prefix, time_next_call,
+                     FrameClassifier, framed_request_prefix, framed_response_prefix)
 from ._lib import (SRPC_ERR_BOUNDS, SRPC_PATH_DWORD, SRPC_PATH_TILE, SRPC_PATH_VAR, SRPC_STATUS_BOUNDS,
                    SRPC_STATUS_PREFIX, UnpackStatus)
 
@@ -21,4 +22,4 @@ __all__ = ["GpuPacker", "Schema", "SrpcError", "fill_splitmix_i32", "time_next_c
            "CHAR", "INT16", "INT32", "INT64", "STRING", "RPC_SUCCESS",
            "RPC_ERR_FUNCTION_NOT_REGISTERED", "RPC_ERR_RECV_TIMEOUT", "SRPC_ERR_BOUNDS",
            "SRPC_PATH_DWORD", "SRPC_PATH_TILE", "SRPC_PATH_VAR", "SRPC_STATUS_BOUNDS", "SRPC_STATUS_PREFIX",
-           "UnpackStatus"]
+           "UnpackStatus", "FrameClassifier", "framed_request_prefix", "framed_response_prefix"]

@@ -59,6 +59,11 @@ SIGNATURES = {
     "srpc_gather_wire": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, C.c_int, _vp]),
     "srpc_group_gather_wire": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _u64, C.c_int, _vp]),
     "srpc_group_pack_gather": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _u64, C.c_int, _vp]),
+    "srpc_frames_scratch_bytes": (C.c_int, [_u64, C.c_int, C.POINTER(_u64)]),
+    "srpc_frames_classify": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64,
+                                       _vp]),
+    "srpc_frames_gather": (C.c_int, [_vp, _vp, _vp, _u64, C.c_uint32, _vp, _vp]),
+    "srpc_frames_scatter": (C.c_int, [_vp, _vp, _u64, C.c_uint32, _vp, _vp, _vp]),
     "srpc_status_string": (C.c_char_p, [C.c_int]),
     "srpc_gpu_abi_version": (C.c_int, []),
 }

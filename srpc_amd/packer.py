@@ -259,6 +259,55 @@ def time_next_call(start=None, stop=None) -> None:
     check(_lib.lib().srpc_time_next_call(handle(start), handle(stop)), "srpc_time_next_call")
 
 
+def framed_request_prefix(schema: Schema, method: str) -> bytes:
+    """``BE32 payload | str(method) | str(T::name)``: the constant head of every
+    frame Calculator_stub-style clients send for a fixed-size request
+    (transport.hpp send_data + packer.hpp:77-82)."""
+    pre = request_prefix(method, schema.name)
+    return struct.pack(">I", len(pre) + schema.body_bytes) + pre
+
+
+def framed_response_prefix(schema: Schema, code: int = RPC_SUCCESS) -> bytes:
+    pre = response_prefix(code, schema.name)
+    return struct.pack(">I", len(pre) + schema.body_bytes) + pre
+
+
+class FrameClassifier:
+    """Buckets a batch of socket frames by method on the device
+    (srpc_frames_classify / _gather / _scatter): ``methods`` is a list of
+    (request GpuPacker with a framed prefix, response record bytes)."""
+
+    def __init__(self, methods: Sequence[tuple["GpuPacker", int]]):
+        self.methods = list(methods)
+        k = len(self.methods)
+        self._plans = (C.c_void_p * k)(*[m[0]._h.value for m in self.methods])
+        self._rb = (C.c_uint32 * k)(*[int(m[1]) for m in self.methods])
+
+    def scratch_bytes(self, nframes: int) -> int:
+        out = C.c_uint64()
+        check(_lib.lib().srpc_frames_scratch_bytes(nframes, len(self.methods), C.byref(out)),
+              "srpc_frames_scratch_bytes")
+        return out.value
+
+    def classify(self, buf, buf_len: int, offs, nframes: int, cls, index, counts, out_off, scratch,
+                 scratch_bytes: int, stream=None) -> None:
+        check(_lib.lib().srpc_frames_classify(self._plans, self._rb, len(self.methods), _dptr(buf), buf_len,
+                                              _dptr(offs), nframes, _dptr(cls), _dptr(index), _dptr(counts),
+                                              _dptr(out_off), _dptr(scratch), scratch_bytes, _stream(stream)),
+              "srpc_frames_classify")
+
+    @staticmethod
+    def gather(buf, offs, index, n: int, record_bytes: int, out, stream=None) -> None:
+        check(_lib.lib().srpc_frames_gather(_dptr(buf), _dptr(offs), _dptr(index), n, record_bytes, _dptr(out),
+                                            _stream(stream)), "srpc_frames_gather")
+
+    @staticmethod
+    def scatter(resp, index, n: int, record_bytes: int, out_off, out, stream=None) -> None:
+        check(_lib.lib().srpc_frames_scatter(_dptr(resp), _dptr(index), n, record_bytes, _dptr(out_off),
+                                             _dptr(out), _stream(stream)), "srpc_frames_scatter")
+
+
 __all__ = ["Schema", "GpuPacker", "SrpcError", "request_prefix", "response_prefix",
-           "fill_splitmix_i32", "time_next_call", "BOOL", "INT8", "CHAR", "INT16", "INT32", "INT64", "STRING",
+           "fill_splitmix_i32", "time_next_call", "framed_request_prefix", "framed_response_prefix",
+           "FrameClassifier", "BOOL", "INT8", "CHAR", "INT16", "INT32", "INT64", "STRING",
            "RPC_SUCCESS", "RPC_ERR_FUNCTION_NOT_REGISTERED", "RPC_ERR_RECV_TIMEOUT"]

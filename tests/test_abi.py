@@ -37,7 +37,7 @@ def test_library_exports_every_symbol():
 
 def test_library_loads_and_answers_host_calls():
     L = _lib.lib()
-    assert L.srpc_gpu_abi_version() == 2
+    assert L.srpc_gpu_abi_version() == 3
     assert L.srpc_status_string(-2) == b"device pointer misaligned"
     assert L.srpc_status_string(2).startswith(b"wire shorter")
     # argument validation needs no device
@@ -48,6 +48,15 @@ def test_library_loads_and_answers_host_calls():
     assert L.srpc_time_next_call(None, None) == _lib.SRPC_OK
     assert L.srpc_time_next_call(C.c_void_p(1), None) == _lib.SRPC_OK
     assert L.srpc_gpu_pack(None, None, 0, None, 0, None) == _lib.SRPC_E_INVALID
+    # frame bucketing: scratch sizing is host arithmetic; bad plan counts are refused
+    out = C.c_uint64()
+    assert L.srpc_frames_scratch_bytes(1 << 20, 4, C.byref(out)) == _lib.SRPC_OK and out.value >= 4 << 20
+    assert L.srpc_frames_scratch_bytes(10, 0, C.byref(out)) == _lib.SRPC_E_INVALID
+    assert L.srpc_frames_scratch_bytes(10, 17, C.byref(out)) == _lib.SRPC_E_INVALID
+    assert L.srpc_frames_classify(None, None, 1, None, 0, None, 0, None, None, None, None, None, 0,
+                                  None) == _lib.SRPC_E_INVALID
+    assert L.srpc_frames_gather(None, None, None, 0, 57, None, None) == _lib.SRPC_OK  # nothing to do
+    assert L.srpc_frames_gather(None, None, None, 3, 57, None, None) == _lib.SRPC_E_INVALID
 
 
 def test_library_is_gfx950_code_object():

@@ -22,23 +22,81 @@ def _run(*args, timeout=300):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+def _served(r, n):
+    g = r["gpu"]
+    assert r["ok"], r
+    assert g["gpu_requests"] + g["fallback_requests"] == n, r
+    return g
+
+
 def test_e2e_square_gpu_batches_small():
     r = _run("--mode", "gpu", "--n", "70001", "--batch", "16384", "--port", "18301")
-    assert r["ok"] and r["gpu"]["fallback_requests"] == 0 and r["gpu"]["batches"] >= 5
+    g = _served(r, 70001)
+    assert g["fallback_requests"] == 0 and g["batches"] >= 5 and g["mixed_batches"] == 0
 
 
-def test_e2e_square_fallback_on_foreign_frame():
+def test_e2e_square_only_the_foreign_frame_leaves_the_gpu():
     r = _run("--mode", "gpu", "--n", "50000", "--batch", "8192", "--port", "18302", "--poison", "12345")
-    assert r["ok"] and r["gpu"]["fallback_requests"] >= 1
+    assert _served(r, 50000)["fallback_requests"] == 1
 
 
-def test_e2e_square_fallback_on_foreign_frame_of_other_length():
-    """A foreign frame 7 bytes longer moves every later frame off the 57-byte
-    grid: the rest of its batch and the bytes already read for the next batch
-    are answered on the CPU, after which batching resumes."""
+def test_e2e_square_foreign_frame_of_other_length():
+    """A foreign frame 7 bytes longer is still one frame: the CPU walks the
+    BE32 lengths, so every later frame stays on the GPU."""
     r = _run("--mode", "gpu", "--n", "50000", "--batch", "8192", "--port", "18304", "--poison", "20000",
              "--poison-method", "Calculator_servicer::square_v2")
-    assert r["ok"] and r["gpu"]["fallback_requests"] >= 1
+    assert _served(r, 50000)["fallback_requests"] == 1
+
+
+def test_e2e_square_poison_at_index_0_of_a_256k_batch():
+    n = 1 << 18
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", str(n), "--port", "18305", "--poison", "0")
+    g = _served(r, n)
+    assert g["fallback_requests"] == 1 and g["gpu_requests"] == n - 1
+    print(json.dumps(r))
+
+
+def test_e2e_one_percent_foreign_traffic():
+    """1 % divide requests (a method the GPU server does not have) among
+    squares: exactly those go to the CPU server, answered in their places."""
+    n = 200_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "65536", "--port", "18306", "--foreign", "0.01")
+    g = _served(r, n)
+    assert 1500 < r["traffic"]["divide"] < 2500
+    assert g["fallback_requests"] == r["traffic"]["divide"]
+    print(json.dumps(r))
+
+
+def test_e2e_mixed_methods_all_on_the_gpu():
+    """square + add / subtract / multiply (two frame lengths) in one stream,
+    all four registered on the GPU: bucketed per method, nothing on the CPU."""
+    n = 120_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "32768", "--port", "18307", "--mix", "0.3",
+             "--gpu-methods", "all")
+    g = _served(r, n)
+    assert g["fallback_requests"] == 0 and g["mixed_batches"] >= 1
+    assert min(r["traffic"][m] for m in ("add", "subtract", "multiply")) > 5000
+
+
+def test_e2e_mixed_methods_some_on_the_cpu():
+    n = 60_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "16384", "--port", "18308", "--mix", "0.2",
+             "--foreign", "0.05", "--poison", "0,17,59999")
+    g = _served(r, n)
+    t = r["traffic"]
+    assert g["fallback_requests"] == t["add"] + t["subtract"] + t["multiply"] + t["divide"] + t["poison"]
+    assert t["poison"] == 3
+
+
+@pytest.mark.parametrize("at", [0, 3000])
+def test_e2e_frame_larger_than_the_batch_buffer(at):
+    """A frame longer than the whole receive buffer is read on its own and
+    answered on the CPU; the connection carries on."""
+    n = 20_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "4096", "--port", str(18309 + at % 7), "--oversize",
+             str(at), "--poison", "5000")
+    g = _served(r, n)
+    assert g["oversize_requests"] == 1 and g["fallback_requests"] == 2
 
 
 @pytest.mark.slow

@@ -1,25 +1,39 @@
 // e2e_square: BASELINE.json configs[4] -- Calculator.square end to end over
-// loopback, 1M requests, server-side GPU-batched unpack -> square -> pack.
+// loopback, 1M requests, server-side GPU-batched unpack -> square -> pack --
+// and the same server under mixed traffic.
 //
 // One process, two threads talking over 127.0.0.1:
-//   client: the frames Calculator_stub::square sends (calculator_srpc.cpp:120-134:
-//           pack_request("Calculator_servicer::square", Number) + u32 BE length),
-//           all N pipelined on one connection by a sender thread, responses
-//           read back and checked against num^2 and (optionally) written out
-//           so their SHA-256 can be compared with the reference digest;
+//   client: the frames Calculator_stub sends (calculator_srpc.cpp:58-134:
+//           pack_request("Calculator_servicer::<m>", Number | TwoNumbers) +
+//           u32 BE length), all N pipelined on one connection by a sender
+//           thread, responses read back and checked against the method's
+//           result and (optionally) written out so their SHA-256 can be
+//           compared with the reference digest;
 //   server: --mode gpu: srpc::gpu::batch_server (include/srpc/gpu_server.hpp)
+//                       with square (and with --gpu-methods all: add, subtract,
+//                       multiply) on the GPU, the rest on the CPU server;
 //           --mode cpu: the scalar srpc::server (include/srpc/server.hpp),
 //                       the reference's per-request dispatch path.
-// Inputs: num = splitmix64(0x5EED) % 46341.  Prints one JSON line.
+// Traffic: num = splitmix64(0x5EED) % 46341 for square;
+//   --mix F      a fraction F of add / subtract / multiply requests (TwoNumbers);
+//   --foreign F  a fraction F of divide requests (a method the GPU server does
+//                not have: answered by the CPU server in their places);
+//   --poison i[,j..]   requests with an unknown method name (NOT_REGISTERED);
+//   --poison-method    the name used (another length moves every later frame);
+//   --oversize i       request i has a method name longer than the batch buffer.
+// Prints one JSON line.
 #include <hip/hip_runtime.h>
 #include <srpc/gpu_server.hpp>
 #include <srpc/server.hpp>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <set>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,27 +48,76 @@ struct Number : public srpc::message_base {
     }
 };
 
-struct Calculator_servicer : srpc::servicer_base {
-    virtual Number square(Number&) { throw std::runtime_error("Method not implemented!"); }
-    static constexpr const char* name = "Calculator";
-    static constexpr auto methods =
-        std::make_tuple(STRUCT_MEMBER(Calculator_servicer, square, "Calculator_servicer::square"));
-};
-
-struct Calculator : Calculator_servicer {
-    Number square(Number& req) override {
-        Number r;
-        r.num = static_cast<int32_t>(static_cast<uint32_t>(req.num) * static_cast<uint32_t>(req.num));
-        return r;
+struct TwoNumbers : public srpc::message_base {
+    int32_t left;
+    int32_t right;
+    static constexpr const char* name = "TwoNumbers";
+    static constexpr auto fields = std::make_tuple(STRUCT_MEMBER(TwoNumbers, left, "TwoNumbers::left"),
+                                                   STRUCT_MEMBER(TwoNumbers, right, "TwoNumbers::right"));
+    void unpack(srpc::buffer::ptr bp) override {
+        srpc::packer p(bp);
+        p >> left;
+        p >> right;
     }
 };
 
-// The batched method on the device: one int32 column in, one out.
+enum Op : int { SQUARE = 0, ADD = 1, SUB = 2, MUL = 3, DIV = 4, POISON = 5, OVERSIZE = 6 };
+
+static int32_t expect(int op, int32_t l, int32_t r) {
+    const uint32_t a = static_cast<uint32_t>(l), b = static_cast<uint32_t>(r);
+    switch (op) {
+        case SQUARE: return static_cast<int32_t>(a * a);
+        case ADD: return static_cast<int32_t>(a + b);
+        case SUB: return static_cast<int32_t>(a - b);
+        case MUL: return static_cast<int32_t>(a * b);
+        default: return l / r;
+    }
+}
+
+struct Calculator_servicer : srpc::servicer_base {
+    virtual Number add(TwoNumbers&) { throw std::runtime_error("Method not implemented!"); }
+    virtual Number subtract(TwoNumbers&) { throw std::runtime_error("Method not implemented!"); }
+    virtual Number multiply(TwoNumbers&) { throw std::runtime_error("Method not implemented!"); }
+    virtual Number divide(TwoNumbers&) { throw std::runtime_error("Method not implemented!"); }
+    virtual Number square(Number&) { throw std::runtime_error("Method not implemented!"); }
+    static constexpr const char* name = "Calculator";
+    static constexpr auto methods =
+        std::make_tuple(STRUCT_MEMBER(Calculator_servicer, add, "Calculator_servicer::add"),
+                        STRUCT_MEMBER(Calculator_servicer, subtract, "Calculator_servicer::subtract"),
+                        STRUCT_MEMBER(Calculator_servicer, multiply, "Calculator_servicer::multiply"),
+                        STRUCT_MEMBER(Calculator_servicer, divide, "Calculator_servicer::divide"),
+                        STRUCT_MEMBER(Calculator_servicer, square, "Calculator_servicer::square"));
+};
+
+struct Calculator : Calculator_servicer {
+    static Number num(int32_t v) {
+        Number r;
+        r.num = v;
+        return r;
+    }
+    Number add(TwoNumbers& q) override { return num(expect(ADD, q.left, q.right)); }
+    Number subtract(TwoNumbers& q) override { return num(expect(SUB, q.left, q.right)); }
+    Number multiply(TwoNumbers& q) override { return num(expect(MUL, q.left, q.right)); }
+    Number divide(TwoNumbers& q) override { return num(expect(DIV, q.left, q.right)); }
+    Number square(Number& q) override { return num(expect(SQUARE, q.num, 0)); }
+};
+
+// The batched methods on the device: int32 columns in, one out.
 __global__ void k_square(const int32_t* __restrict__ in, int32_t* __restrict__ out, uint64_t n) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < n) {
         const uint32_t v = static_cast<uint32_t>(in[i]);
         out[i] = static_cast<int32_t>(v * v);
+    }
+}
+
+template <int OP>
+__global__ void k_binop(const int32_t* __restrict__ l, const int32_t* __restrict__ r, int32_t* __restrict__ out,
+                        uint64_t n) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t a = static_cast<uint32_t>(l[i]), b = static_cast<uint32_t>(r[i]);
+        out[i] = static_cast<int32_t>(OP == ADD ? a + b : OP == SUB ? a - b : a * b);
     }
 }
 
@@ -65,6 +128,15 @@ static int square_batch(void* const* req, void* const* resp, uint64_t n, hipStre
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+template <int OP>
+static int binop_batch(void* const* req, void* const* resp, uint64_t n, hipStream_t s) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_binop<OP>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
+                       static_cast<const int32_t*>(req[0]), static_cast<const int32_t*>(req[1]),
+                       static_cast<int32_t*>(resp[0]), n);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 static uint64_t splitmix(uint64_t* s) {
     uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -72,12 +144,27 @@ static uint64_t splitmix(uint64_t* s) {
     return z ^ (z >> 31);
 }
 
+template <typename T>
+static void append_frame(std::vector<uint8_t>& frames, std::string const& method, T&& v) {
+    srpc::packer pr;
+    srpc::request_t<std::decay_t<T>> req;
+    req.set_method_name(method);
+    req.set_value(std::forward<T>(v));
+    pr.pack_request(req);
+    const uint32_t len = htonl(static_cast<uint32_t>(pr.size()));
+    const uint8_t* lb = reinterpret_cast<const uint8_t*>(&len);
+    frames.insert(frames.end(), lb, lb + 4);
+    frames.insert(frames.end(), pr.data(), pr.data() + pr.size());
+}
+
 int main(int argc, char** argv) {
     uint64_t n = 1u << 20;
     uint64_t batch = 1u << 18;
-    std::string mode = "gpu", port = "18090", dump;
-    int64_t poison = -1;  // request index sent with an unknown method (exercises the CPU fallback)
-    std::string poison_method = "Calculator_servicer::squarX";  // same frame length as the real one
+    std::string mode = "gpu", port = "18090", dump, gpu_methods = "square";
+    std::set<uint64_t> poison;
+    std::string poison_method = "Calculator_servicer::squarX";  // same frame length as square's
+    int64_t oversize = -1;
+    double mix = 0, foreign = 0;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -86,44 +173,79 @@ int main(int argc, char** argv) {
         else if (a == "--mode") mode = next();
         else if (a == "--port") port = next();
         else if (a == "--dump") dump = next();
-        else if (a == "--poison") poison = std::stoll(next());
-        else if (a == "--poison-method") poison_method = next();  // another length shifts every later frame
+        else if (a == "--poison") {
+            std::stringstream ss(next());
+            for (std::string t; std::getline(ss, t, ',');) poison.insert(std::stoull(t));
+        } else if (a == "--poison-method") poison_method = next();
+        else if (a == "--oversize") oversize = std::stoll(next());
+        else if (a == "--mix") mix = std::stod(next());
+        else if (a == "--foreign") foreign = std::stod(next());
+        else if (a == "--gpu-methods") gpu_methods = next();
     }
     srpc::message_registry["Number"] = []() -> std::unique_ptr<Number> { return std::make_unique<Number>(); };
-
-    // ---- client-side request frames, exactly as the stub builds them -------
-    std::vector<int32_t> nums(n);
-    uint64_t st = 0x5EED;
-    for (uint64_t i = 0; i < n; ++i) {
-        const int32_t v = static_cast<int32_t>(static_cast<uint32_t>(splitmix(&st)));
-        nums[i] = v % 46341;
-    }
-    std::vector<uint8_t> frames;
-    frames.reserve(n * 57);
-    for (uint64_t i = 0; i < n; ++i) {
-        srpc::packer pr;
-        srpc::request_t<Number> req;
-        req.set_method_name(static_cast<int64_t>(i) == poison ? poison_method : "Calculator_servicer::square");
-        Number v;
-        v.num = nums[i];
-        req.set_value(std::move(v));
-        pr.pack_request(req);
-        const uint32_t len = htonl(static_cast<uint32_t>(pr.size()));
-        const uint8_t* lb = reinterpret_cast<const uint8_t*>(&len);
-        frames.insert(frames.end(), lb, lb + 4);
-        frames.insert(frames.end(), pr.data(), pr.data() + pr.size());
-    }
-    const uint64_t resp_frame = 4 + 19;
+    srpc::message_registry["TwoNumbers"] = []() -> std::unique_ptr<TwoNumbers> {
+        return std::make_unique<TwoNumbers>();
+    };
 
     // ---- server ------------------------------------------------------------
     Calculator calc;
     srpc::server cpu_server;
     cpu_server.register_service(calc);
-    std::unique_ptr<srpc::gpu::batch_server<Number, Number>> gsrv;
+    std::unique_ptr<srpc::gpu::batch_server> gsrv;
+    uint64_t buffer_bytes = 0;
     if (mode == "gpu") {
-        gsrv = std::make_unique<srpc::gpu::batch_server<Number, Number>>("Calculator_servicer::square", square_batch,
-                                                                         batch, 0, &cpu_server);
+        gsrv = srpc::gpu::batch_server::single<Number, Number>("Calculator_servicer::square", square_batch, batch, 0,
+                                                               &cpu_server);
+        if (gpu_methods == "all") {
+            gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::add", binop_batch<ADD>);
+            gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::subtract", binop_batch<SUB>);
+            gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::multiply", binop_batch<MUL>);
+        }
+        buffer_bytes = gsrv->buffer_bytes();
     }
+
+    // ---- client-side request frames, exactly as the stub builds them -------
+    std::vector<int32_t> lhs(n), rhs(n);
+    std::vector<uint8_t> ops(n);
+    uint64_t st = 0x5EED, st2 = 0xF00D;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int32_t v = static_cast<int32_t>(static_cast<uint32_t>(splitmix(&st)));
+        lhs[i] = v % 46341;
+        const double u = static_cast<double>(splitmix(&st2) >> 11) * 0x1.0p-53;
+        const uint64_t w = splitmix(&st2);
+        ops[i] = u < foreign ? DIV : u < foreign + mix ? static_cast<uint8_t>(ADD + w % 3) : SQUARE;
+        rhs[i] = ops[i] == DIV ? static_cast<int32_t>(w >> 40) % 1000 + 1 : static_cast<int32_t>(w >> 32);
+        if (poison.count(i)) ops[i] = POISON;
+        if (static_cast<int64_t>(i) == oversize) ops[i] = OVERSIZE;
+    }
+    static const char* kName[] = {"Calculator_servicer::square", "Calculator_servicer::add",
+                                  "Calculator_servicer::subtract", "Calculator_servicer::multiply",
+                                  "Calculator_servicer::divide"};
+    std::vector<uint8_t> frames;
+    frames.reserve(n * 62);
+    uint64_t counts[7] = {};
+    uint64_t resp_total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int op = ops[i];
+        counts[op] += 1;
+        if (op == SQUARE || op == POISON) {
+            Number v;
+            v.num = lhs[i];
+            append_frame(frames, op == POISON ? poison_method : kName[SQUARE], std::move(v));
+        } else if (op == OVERSIZE) {
+            Number v;
+            v.num = lhs[i];
+            append_frame(frames, std::string(std::max<uint64_t>(buffer_bytes, 4096) + 1000, 'Z'), std::move(v));
+        } else {
+            TwoNumbers v;
+            v.left = lhs[i];
+            v.right = rhs[i];
+            append_frame(frames, kName[op], std::move(v));
+        }
+        // an unknown method is answered with the one status byte RPC_ERR_FUNCTION_NOT_REGISTERED
+        resp_total += op == POISON || op == OVERSIZE ? 5 : 23;
+    }
+
     const int lfd = srpc::transport::create_server_socket(port);
     if (lfd < 0) return 3;
     srpc::gpu::batch_stats stats;
@@ -146,8 +268,6 @@ int main(int argc, char** argv) {
     int big = 8 << 20;
     setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof(big));
     setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
-    // an unknown method is answered with the one status byte RPC_ERR_FUNCTION_NOT_REGISTERED
-    const uint64_t resp_total = n * resp_frame - (poison >= 0 && static_cast<uint64_t>(poison) < n ? 18 : 0);
     std::vector<uint8_t> resp(resp_total);
     auto t0 = std::chrono::steady_clock::now();
     std::thread sender([&] { srpc::transport::send_all(fd, frames.data(), frames.size()); });
@@ -165,34 +285,45 @@ int main(int argc, char** argv) {
     const uint8_t* f = resp.data();
     for (uint64_t i = 0; got_all && i < n; ++i) {
         const uint32_t len = (uint32_t(f[0]) << 24) | (uint32_t(f[1]) << 16) | (uint32_t(f[2]) << 8) | f[3];
-        if (static_cast<int64_t>(i) == poison) {
+        if (ops[i] == POISON || ops[i] == OVERSIZE) {
             if (len != 1 || f[4] != srpc::RPC_ERR_FUNCTION_NOT_REGISTERED) ++bad;
             f += 5;
             continue;
         }
+        if (len != 19) {
+            ++bad;
+            break;  // the stream is out of step from here on
+        }
         srpc::packer rpr(f + 4, len);
         f += 4 + len;
         srpc::response_t<Number> m = rpr.unpack_response<Number>();
-        if (len != 19 || m.code() != srpc::RPC_SUCCESS ||
-            m.value().num != static_cast<int32_t>(static_cast<uint32_t>(nums[i]) * static_cast<uint32_t>(nums[i])))
-            ++bad;
+        if (m.code() != srpc::RPC_SUCCESS || m.value().num != expect(ops[i], lhs[i], rhs[i])) ++bad;
     }
-    if (!dump.empty() && got_all && poison < 0) {  // unframed responses, for the reference digest
+    const bool pure = poison.empty() && oversize < 0 && counts[SQUARE] == n;
+    if (!dump.empty() && got_all && pure) {  // unframed responses, for the reference digest
         FILE* fp = std::fopen(dump.c_str(), "wb");
-        for (uint64_t i = 0; fp && i < n; ++i) std::fwrite(resp.data() + i * resp_frame + 4, 1, 19, fp);
+        for (uint64_t i = 0; fp && i < n; ++i) std::fwrite(resp.data() + i * 23 + 4, 1, 19, fp);
         if (fp) std::fclose(fp);
     }
     std::printf(
-        "{\"workload\": \"Calculator.square e2e over 127.0.0.1, one connection, pipelined\", \"mode\": \"%s\", "
+        "{\"workload\": \"Calculator e2e over 127.0.0.1, one connection, pipelined\", \"mode\": \"%s\", "
         "\"requests\": %llu, \"ok\": %s, \"bad\": %llu, \"seconds\": %.6f, \"requests_per_s\": %.1f, "
-        "\"request_frame_bytes\": 57, \"response_frame_bytes\": 23, \"wire_in_MBps\": %.1f, "
-        "\"gpu\": {\"batches\": %llu, \"batch_frames\": %llu, \"fallback_requests\": %llu, "
-        "\"gpu_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, \"recv_seconds\": %.6f, "
-        "\"send_seconds\": %.6f, \"gpu_requests_per_s\": %.1f}, \"cpu_served\": %zu}\n",
+        "\"request_bytes\": %zu, \"wire_in_MBps\": %.1f, "
+        "\"traffic\": {\"square\": %llu, \"add\": %llu, \"subtract\": %llu, \"multiply\": %llu, \"divide\": %llu, "
+        "\"poison\": %llu, \"oversize\": %llu, \"mix\": %.4f, \"foreign\": %.4f, \"gpu_methods\": \"%s\"}, "
+        "\"gpu\": {\"batches\": %llu, \"mixed_batches\": %llu, \"batch_frames\": %llu, \"buffer_bytes\": %llu, "
+        "\"gpu_requests\": %llu, \"fallback_requests\": %llu, \"oversize_requests\": %llu, "
+        "\"gpu_seconds\": %.6f, \"fallback_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, "
+        "\"recv_seconds\": %.6f, \"send_seconds\": %.6f, \"gpu_requests_per_s\": %.1f}, \"cpu_served\": %zu}\n",
         mode.c_str(), (unsigned long long)n, (got_all && bad == 0) ? "true" : "false", (unsigned long long)bad, secs,
-        n / secs, n * 57.0 / secs / 1e6, (unsigned long long)stats.gpu_batches, (unsigned long long)batch,
-        (unsigned long long)stats.fallback_requests, stats.gpu_seconds, (unsigned long long)stats.h2d_bytes,
-        (unsigned long long)stats.d2h_bytes, stats.recv_seconds, stats.send_seconds,
-        stats.gpu_seconds > 0 ? stats.requests / stats.gpu_seconds : 0.0, cpu_served);
+        n / secs, frames.size(), frames.size() / secs / 1e6, (unsigned long long)counts[SQUARE],
+        (unsigned long long)counts[ADD], (unsigned long long)counts[SUB], (unsigned long long)counts[MUL],
+        (unsigned long long)counts[DIV], (unsigned long long)counts[POISON], (unsigned long long)counts[OVERSIZE], mix,
+        foreign, gpu_methods.c_str(), (unsigned long long)stats.gpu_batches, (unsigned long long)stats.mixed_batches,
+        (unsigned long long)batch, (unsigned long long)buffer_bytes, (unsigned long long)stats.gpu_requests,
+        (unsigned long long)stats.fallback_requests, (unsigned long long)stats.oversize_requests, stats.gpu_seconds,
+        stats.fallback_seconds, (unsigned long long)stats.h2d_bytes, (unsigned long long)stats.d2h_bytes,
+        stats.recv_seconds, stats.send_seconds,
+        stats.gpu_seconds > 0 ? stats.gpu_requests / stats.gpu_seconds : 0.0, cpu_served);
     return (got_all && bad == 0) ? 0 : 1;
 }
