@@ -107,7 +107,16 @@ typedef struct srpc_plan srpc_plan;
 #define SRPC_PATH_VAR 3     /* string fields: per-record sizes + wavefront/device scan   */
 
 /* Validate a schema and prepare its kernels on `device` (allocates the
- * plan's small device-side prefix copy; never called on the hot path). */
+ * plan's small device-side prefix copy; never called on the hot path).
+ * Limits of this build (the reference's pack_struct has none, packer.hpp:
+ * 172-178): at most SRPC_MAX_FIELDS leaf fields after flattening and an
+ * envelope prefix of at most SRPC_MAX_PREFIX bytes -- so a fixed record is at
+ * most 1024 + 32 * 8 = 1280 bytes.  A schema past a limit is refused with
+ * SRPC_E_UNSUPPORTED before any device work; nfields == 0, an unknown kind or
+ * a NULL pointer is SRPC_E_INVALID.  (srpc::gpu::batch_packer<T> throws
+ * srpc::gpu::plan_error carrying the code.) */
+#define SRPC_MAX_FIELDS 32
+#define SRPC_MAX_PREFIX 1024
 int srpc_plan_create(const srpc_schema_desc* desc, int device, srpc_plan** out);
 int srpc_plan_destroy(srpc_plan* plan);
 

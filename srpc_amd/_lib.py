@@ -27,6 +27,8 @@ SRPC_STATUS_PREFIX = 1
 SRPC_STATUS_BOUNDS = 2
 SRPC_STATUS_STALLED = 4
 SRPC_COMM_ID_BYTES = 128
+SRPC_MAX_FIELDS = 32
+SRPC_MAX_PREFIX = 1024
 
 SRPC_PATH_DWORD = 1
 SRPC_PATH_TILE = 2

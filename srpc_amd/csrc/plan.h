@@ -13,11 +13,13 @@
 namespace srpc_impl {
 
 constexpr int kBlock = 256;          // 4 waves of 64
-constexpr int kMaxFields = 32;
+constexpr int kMaxFields = SRPC_MAX_FIELDS;
 constexpr int kMaxDwords = 8;        // DWORD path: records of up to 32 bytes
 constexpr uint32_t kTileTarget = 8192;   // TILE path: ~8 KiB LDS image per tile
 constexpr uint32_t kMaxTileStride = 2048;
-constexpr uint32_t kMaxPrefix = 1024;
+constexpr uint32_t kMaxPrefix = SRPC_MAX_PREFIX;
+// every schema within the limits has a TILE kernel (records of <= 1280 bytes)
+static_assert(kMaxPrefix + 8u * kMaxFields <= kMaxTileStride, "fixed records within the limits fit a tile");
 
 // Variant bits (srpc_plan_tune SRPC_TUNE_NT): non-temporal stores / loads.
 constexpr int kNtStore = 1;

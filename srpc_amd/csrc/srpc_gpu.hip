@@ -862,9 +862,8 @@ const char* srpc_status_string(int code) {
 int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
     if (!d || !out) return SRPC_E_INVALID;
     *out = nullptr;
-    if (d->nfields == 0 || d->nfields > static_cast<uint32_t>(kMaxFields) || !d->kinds)
-        return SRPC_E_INVALID;
-    if (d->prefix_len > kMaxPrefix || (d->prefix_len && !d->prefix)) return SRPC_E_INVALID;
+    if (d->nfields == 0 || !d->kinds || (d->prefix_len && !d->prefix)) return SRPC_E_INVALID;
+    if (d->nfields > static_cast<uint32_t>(kMaxFields) || d->prefix_len > kMaxPrefix) return SRPC_E_UNSUPPORTED;
     auto* p = new (std::nothrow) srpc_plan();
     if (!p) return SRPC_E_INVALID;
     p->device = device;

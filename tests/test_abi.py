@@ -48,6 +48,14 @@ def test_library_loads_and_answers_host_calls():
     assert L.srpc_time_next_call(None, None) == _lib.SRPC_OK
     assert L.srpc_time_next_call(C.c_void_p(1), None) == _lib.SRPC_OK
     assert L.srpc_gpu_pack(None, None, 0, None, 0, None) == _lib.SRPC_E_INVALID
+    # schema limits (SRPC_MAX_FIELDS, SRPC_MAX_PREFIX) are refused before any device work
+    kinds33 = (C.c_int32 * 33)(*([5] * 33))
+    h = C.c_void_p()
+    assert L.srpc_plan_create(C.byref(_lib.SchemaDesc(33, kinds33, None, 0)), 0, C.byref(h)) == _lib.SRPC_E_UNSUPPORTED
+    pre = (C.c_uint8 * 1025)()
+    assert L.srpc_plan_create(C.byref(_lib.SchemaDesc(1, kinds33, pre, 1025)), 0, C.byref(h)) == \
+        _lib.SRPC_E_UNSUPPORTED
+    assert L.srpc_plan_create(C.byref(_lib.SchemaDesc(0, kinds33, None, 0)), 0, C.byref(h)) == _lib.SRPC_E_INVALID
     # frame bucketing: scratch sizing is host arithmetic; bad plan counts are refused
     out = C.c_uint64()
     assert L.srpc_frames_scratch_bytes(1 << 20, 4, C.byref(out)) == _lib.SRPC_OK and out.value >= 4 << 20

@@ -30,6 +30,15 @@ def test_reference_generated_stub_links_unchanged():
     assert "ok" in _run("calculator_compat_test")
 
 
+def test_cpp_schema_limits_refused():
+    """33 leaf fields or a 1025-byte envelope: batch_packer<T> throws plan_error
+    with SRPC_E_UNSUPPORTED (refused before any device work, so no GPU needed)."""
+    from srpc_amd import build
+    build.build()
+    out = _run("schema_limits_test")
+    assert "0 failed" in out and out.count("refused:") == 3
+
+
 @pytest.mark.gpu
 def test_cpp_gpu_batch_packer():
     torch = pytest.importorskip("torch")

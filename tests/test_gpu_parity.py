@@ -167,6 +167,42 @@ def test_random_schemas_vs_oracle(n, schema):
             assert a.tobytes() == b.tobytes()
 
 
+@pytest.mark.parametrize("n", [1, 1000, 20_001])
+@pytest.mark.parametrize("strings", [False, True])
+def test_schema_at_the_limits_vs_oracle(n, strings):
+    """SRPC_MAX_FIELDS leaf fields behind a SRPC_MAX_PREFIX-byte envelope (the
+    widest schema this build accepts; one more field or prefix byte is refused,
+    tests/test_abi.py): a 1280-byte fixed record on the TILE path, and the same
+    with every fourth field a string on the VAR path."""
+    kinds = [[oracle.INT64, oracle.INT8, oracle.INT32, oracle.INT16][i % 4] for i in range(srpc_amd._lib.SRPC_MAX_FIELDS)]
+    if strings:
+        kinds = [oracle.STRING if i % 4 == 1 else k for i, k in enumerate(kinds)]
+    rng = np.random.default_rng(n)
+    prefix = rng.integers(0, 256, srpc_amd._lib.SRPC_MAX_PREFIX, dtype=np.uint8).tobytes()
+    p = GpuPacker(Schema("Wide", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    if not strings:
+        assert p.path == SRPC_PATH_TILE and p.record_bytes == 1024 + 8 * 8 + 8 * 1 + 8 * 4 + 8 * 2
+        cols = [rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(oracle.KIND_DTYPE[k])
+                for k in kinds]
+        want = oracle.pack(kinds, cols, n, prefix)
+        assert gpu_pack(p, cols, n) == want
+        rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+        assert rc == 0 and all(a.tobytes() == b.tobytes() for a, b in zip(cols, back))
+        return
+    cols, offs = _random_string_batch(kinds, n, rng, 24)
+    want = oracle.pack(kinds, cols, n, prefix, list(offs))
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st == (0, 2**64 - 1) and wire == bytes(want)
+    back, boffs, st = gpu_unpack_var(p, kinds, wire, n, rec)
+    assert st[0] == 0
+    rc, ocols, ooffs, _, _ = oracle.unpack(kinds, want, n, prefix)
+    assert rc == 0
+    for f, k in enumerate(kinds):
+        assert back[f].tobytes() == ocols[f].tobytes(), f
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f], ooffs[f]), f
+
+
 @pytest.mark.parametrize("schema", ["quad", "number", "two", "i64x2"])
 def test_dword_variants_identical(schema):
     sch = {"quad": QUAD, "number": NUMBER, "two": TWO_NUMBERS,
