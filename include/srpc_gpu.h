@@ -138,8 +138,9 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
                                         (1024..49152), pack and unpack           */
 #define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
 #define SRPC_TUNE_VAR_KERNEL 7       /* VAR: 1 = record tiles, one pass (default; unpack of
-                                        multi-string schemas keeps 0), 0 = offset scans +
-                                        chunk walks, 2 = record tiles for every unpack */
+                                        records under 40 bytes on average keeps 0), 0 =
+                                        offset scans + chunk walks, 2 = record tiles for
+                                        every unpack */
 #define SRPC_TUNE_VAR_IMAGE_BYTES 8  /* VAR record tiles: LDS image bytes (8192..65536,
                                         multiple of 16); larger tiles take the walk  */
 #define SRPC_TUNE_VAR_CHARS_BYTES 10 /* VAR record tiles: LDS chars stage bytes

@@ -115,6 +115,48 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
     }
 }
 
+// ---- LDS byte access with aligned instructions (every file's kernels) ----
+// The k <= 8 low bytes of v at LDS byte d, each byte written once, with the
+// widest naturally aligned stores that fit.
+__device__ __forceinline__ void lds_put_small(uint8_t* lds, uint32_t d, uint64_t v, uint32_t k) {
+    if (k && (d & 1)) {
+        lds[d] = static_cast<uint8_t>(v);
+        v >>= 8;
+        ++d;
+        --k;
+    }
+    if (k >= 2 && (d & 2)) {
+        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
+        v >>= 16;
+        d += 2;
+        k -= 2;
+    }
+    while (k >= 4) {
+        *reinterpret_cast<uint32_t*>(lds + d) = static_cast<uint32_t>(v);
+        v >>= 32;
+        d += 4;
+        k -= 4;
+    }
+    if (k >= 2) {
+        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
+        v >>= 16;
+        d += 2;
+        k -= 2;
+    }
+    if (k) lds[d] = static_cast<uint8_t>(v);
+}
+
+// 8 bytes at any LDS byte offset from three aligned dword reads and two byte
+// funnel shifts: a misaligned ds_read_b64 costs ~6x an aligned one on gfx950
+// (profiles/r01_lds_unaligned.log).  Reads up to 4 bytes past the value,
+// inside the LDS allocation.
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t* lds, uint32_t off) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (off & ~3u));
+    const uint32_t s = off & 3;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, s)) << 32) | __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+
 }  // namespace srpc_impl
 
 // The object behind the opaque srpc_plan* of include/srpc_gpu.h.
@@ -147,7 +189,7 @@ struct srpc_plan {
     uint32_t nstrings = 0;
     uint32_t fixed_bytes = 0;        // prefix + fixed fields + 8 per string field
     int var_kernel = 1;              // SRPC_TUNE_VAR_KERNEL: 1 record tiles (one pass), 0 scan + chunk walk
-    bool var_rt_general = false;     // unpack: record tiles with the look-back for multi-string schemas too (A/B)
+    bool var_rt_general = false;     // unpack: record tiles for short records too (A/B)
     uint32_t rt_img_cap = 0;         // record tiles: LDS image bytes, 0 = from wire_cap / n (SRPC_TUNE_VAR_IMAGE_BYTES)
     uint32_t rt_ch_cap = 0;          // record tiles: LDS chars stage bytes (SRPC_TUNE_VAR_CHARS_BYTES)
     bool rt_ch_cap_auto = true;      //   ... or what the image's span can hold

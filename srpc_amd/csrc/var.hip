@@ -1020,36 +1020,6 @@ constexpr uint64_t kRtuMinAvg = 40;  // record-tile unpack: smallest average rec
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
 typedef uint8_t __attribute__((address_space(3))) lds_u8;
 
-// The k <= 8 low bytes of v at LDS byte d, each byte written once, with the
-// widest naturally aligned stores that fit.
-__device__ __forceinline__ void lds_put_small(uint8_t* lds, uint32_t d, uint64_t v, uint32_t k) {
-    if (k && (d & 1)) {
-        lds[d] = static_cast<uint8_t>(v);
-        v >>= 8;
-        ++d;
-        --k;
-    }
-    if (k >= 2 && (d & 2)) {
-        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
-        v >>= 16;
-        d += 2;
-        k -= 2;
-    }
-    while (k >= 4) {
-        *reinterpret_cast<uint32_t*>(lds + d) = static_cast<uint32_t>(v);
-        v >>= 32;
-        d += 4;
-        k -= 4;
-    }
-    if (k >= 2) {
-        *reinterpret_cast<uint16_t*>(lds + d) = static_cast<uint16_t>(v);
-        v >>= 16;
-        d += 2;
-        k -= 2;
-    }
-    if (k) lds[d] = static_cast<uint8_t>(v);
-}
-
 // LDS bytes [s, s + len) -> LDS bytes [d, d + len): aligned dword stores in
 // the body, each built from two aligned dword loads of the source and a byte
 // funnel shift (the load may read up to 3 bytes past the run, inside the LDS
@@ -1450,6 +1420,68 @@ __device__ __forceinline__ uint32_t parse_record(const VarArgs& a, const uint8_t
     return flag;
 }
 
+// parse_record for a record staged in LDS at byte offset `so` (wire offset
+// `start`), the prefix at LDS offset `po` (16-aligned): every read is aligned.
+__device__ __forceinline__ uint32_t parse_record_lds(const VarArgs& a, const uint8_t* lds, uint32_t so, uint32_t po,
+                                                     uint64_t r, uint64_t start, uint64_t end, uint64_t wire_len,
+                                                     uint64_t* pos_l, uint64_t* len_l, uint32_t i) {
+    uint32_t flag = 0;
+    if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
+    if (!flag && a.prefix_len) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (so & ~3u));
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(lds + po);
+        const uint32_t s = so & 3;
+        uint32_t w0 = w[0], diff = 0;
+        const uint32_t nd = (a.prefix_len + 3) >> 2;
+        for (uint32_t k = 0; k < nd; ++k) {
+            const uint32_t w1 = w[k + 1];
+            const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, s) ^ p[k];
+            const uint32_t left = a.prefix_len - 4 * k;
+            diff |= left >= 4 ? x : (x & ((1u << (8 * left)) - 1));
+            w0 = w1;
+        }
+        if (diff) flag = SRPC_STATUS_PREFIX;
+    }
+    uint64_t pos = start + a.prefix_len;
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            if (flag != SRPC_STATUS_BOUNDS && pos + sz <= end) {
+                const uint64_t v = lds_u64(lds, so + static_cast<uint32_t>(pos - start));
+                uint8_t* dst = const_cast<uint8_t*>(a.col[f]) + r * sz;
+                switch (sz) {
+                case 1: dst[0] = static_cast<uint8_t>(v); break;
+                case 2: *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(v); break;
+                case 4: *reinterpret_cast<uint32_t*>(dst) = static_cast<uint32_t>(v); break;
+                default: *reinterpret_cast<uint64_t*>(dst) = v; break;
+                }
+            }
+            pos += sz;
+            continue;
+        }
+        uint64_t len = 0;
+        if (flag != SRPC_STATUS_BOUNDS && pos + 8 <= end) {
+            len = lds_u64(lds, so + static_cast<uint32_t>(pos - start));
+            pos += 8;
+            if (len > end - pos) {
+                flag = SRPC_STATUS_BOUNDS;
+                len = 0;
+            }
+        } else {
+            flag = SRPC_STATUS_BOUNDS;
+        }
+        pos_l[si * kBlock + i] = pos;
+        len_l[si * kBlock + i] = len;
+        ++si;
+        pos += len;
+    }
+    if (!flag && pos != end) flag = SRPC_STATUS_BOUNDS;  // record size disagrees with the index
+    if (flag == SRPC_STATUS_BOUNDS)
+        for (uint32_t k = 0; k < a.nstrings; ++k) len_l[k * kBlock + i] = 0;
+    return flag;
+}
+
 // kOpt (single-string schemas): no look-back -- when every record is exact
 // (its decoded string length is its index size minus fixed_bytes), string
 // chars of record r start at rec_offs[r] - rec_offs[0] - r * fixed_bytes, so
@@ -1551,7 +1583,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         const uint64_t start = win[i], end = win[i + 1];
         uint32_t flag;
         if (staged && start >= slo && end <= shi && start <= end)
-            flag = parse_record(a, sbase + (start - sw), lds + L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
+            flag = parse_record_lds(a, lds, static_cast<uint32_t>(sbase - lds) + static_cast<uint32_t>(start - sw),
+                                    L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
         else
             flag = parse_record(a, wire + start, lds + L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
         if (flag && st) report_bad(st, flag, r0 + i);
@@ -1620,9 +1653,11 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
             }
         }
     };
-    if (!kOpt && i < 64) {
+    // string field si's look-back runs on wave si mod 4: the fields' round
+    // trips overlap instead of adding up (two strings: one wave each)
+    if (!kOpt && (i >> 6) < ns) {
         bool stalled = false;
-        for (uint32_t si = 0; si < ns; ++si) {
+        for (uint32_t si = i >> 6; si < ns; si += kBlock / 64) {
 #if SRPC_RTU_NOLOOK  // A/B timing only: wrong offsets
             const uint64_t pre = 0;
 #else
@@ -1996,14 +2031,14 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     // record tiles, one pass (default), for batches whose tiles' wire spans fit LDS
     RtuArgs R{};
     uint32_t rlds = 0;
-    // (single-string schemas; multi-string batches keep the walk + scans +
-    // chars kernels: a look-back on the tiles' chars totals made the record
-    // tiles no faster there, profiles/r02_var_rtu_ab.log)
+    // (multi-string schemas look back on the tiles' chars totals, one wave per
+    // string field: two strings + request envelope 358 us with the walk + scans
+    // + chars kernels -> 305 us, profiles/r02_var_rtu_parlook_ab.log)
     // Very short records (under ~40 bytes on average) keep the staged walk +
     // chars kernels as well: their 256-record tiles are too small to pay for a
     // tile's fixed cost (0-16 B strings 104 vs 142 us, 0-32 B 71 vs 88 us;
     // 50-byte records 206 -> 146 us with the tiles, profiles/r02_var_rtu_ab.log).
-    if (p->var_kernel == 1 && (p->nstrings == 1 || p->var_rt_general) &&
+    if (p->var_kernel == 1 &&
         (n == 0 || ((wire_len / n >= kRtuMinAvg || p->var_rt_general) && rtu_layout(p, wire_len / n, &R, &rlds)))) {
         if (n == 0) {
             launch(k_str_offs_zero, dim3(1), dim3(64), 0, s, a);

@@ -11,7 +11,7 @@ TAG=$1
 shift
 for F in "$@"; do
   D=gpurun_out/pmc_${TAG}_$F
-  RUN="python3 tools/bench_paths.py --only $F --reps 3"
+  RUN="python3 tools/bench_paths.py --only $F --reps 3 $PMC_ARGS"
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/stats -o run --output-format csv -- $RUN > $D.stats.log 2>&1 || exit 1
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" \
