@@ -103,19 +103,29 @@ struct host_columns {
 
     void scatter(std::vector<T> const& recs) {
         n = recs.size();
-        col.clear();
-        offs.clear();
+        // the columns are reused from call to call: fresh ones cost a page
+        // fault per 4 KiB on first touch, twice the copy itself (Quad: 12.5
+        // ns per record with new vectors, ~4.5 reused, profiles/r02_host_columns.log)
         T probe{};
+        size_t nf = 0;
+        for_each_leaf<T>(probe, [&](const auto&) { ++nf; });
+        col.resize(nf);
+        offs.resize(nf);
+        size_t g = 0;
         for_each_leaf<T>(probe, [&](const auto& v) {
             using F = std::remove_cvref_t<decltype(v)>;
             if constexpr (std::is_same_v<F, std::string>) {
-                col.emplace_back();
-                offs.emplace_back(1, 0);
+                col[g].clear();
+                offs[g].assign(1, 0);
+                offs[g].reserve(n + 1);
             } else {
-                col.emplace_back(n * sizeof(F));
-                offs.emplace_back();
+                col[g].resize(n * sizeof(F));
+                offs[g].clear();
             }
+            ++g;
         });
+        uint8_t* dst[kMaxLeaves] = {};
+        for (size_t f = 0; f < col.size() && f < kMaxLeaves; ++f) dst[f] = col[f].data();
         for (uint64_t i = 0; i < n; ++i) {
             size_t f = 0;
             for_each_leaf<T>(recs[i], [&](const auto& v) {
@@ -124,7 +134,7 @@ struct host_columns {
                     col[f].insert(col[f].end(), v.begin(), v.end());
                     offs[f].push_back(col[f].size());
                 } else {
-                    std::memcpy(col[f].data() + i * sizeof(F), &v, sizeof(F));
+                    std::memcpy(dst[f] + i * sizeof(F), &v, sizeof(F));
                 }
                 ++f;
             });
@@ -133,6 +143,8 @@ struct host_columns {
 
     void gather(std::vector<T>& recs) const {
         recs.resize(n);
+        const uint8_t* src[kMaxLeaves] = {};
+        for (size_t f = 0; f < col.size() && f < kMaxLeaves; ++f) src[f] = col[f].data();
         for (uint64_t i = 0; i < n; ++i) {
             size_t f = 0;
             for_each_leaf<T>(recs[i], [&](auto& v) {
@@ -140,13 +152,29 @@ struct host_columns {
                 if constexpr (std::is_same_v<F, std::string>) {
                     v.assign(reinterpret_cast<const char*>(col[f].data()) + offs[f][i], offs[f][i + 1] - offs[f][i]);
                 } else {
-                    std::memcpy(&v, col[f].data() + i * sizeof(F), sizeof(F));
+                    std::memcpy(&v, src[f] + i * sizeof(F), sizeof(F));
                 }
                 ++f;
             });
         }
     }
+
+private:
+    static constexpr size_t kMaxLeaves = SRPC_MAX_FIELDS;
 };
+
+/// Byte offset of each leaf field of T inside a T object (T::fields order,
+/// nested messages flattened) -- the field_offsets of srpc_gpu_pack_aos.
+template <SrpcMessage T>
+std::vector<uint32_t> leaf_offsets() {
+    std::vector<uint32_t> o;
+    T probe{};
+    const auto* base = reinterpret_cast<const unsigned char*>(&probe);
+    for_each_leaf<T>(probe, [&](const auto& v) {
+        o.push_back(static_cast<uint32_t>(reinterpret_cast<const unsigned char*>(&v) - base));
+    });
+    return o;
+}
 
 class plan_error : public std::runtime_error {
 public:
@@ -168,7 +196,10 @@ public:
         return batch_packer(response_prefix<T>(code), device);
     }
 
-    batch_packer(batch_packer&& o) noexcept : _plan(o._plan), _nfields(o._nfields), _rb(o._rb) { o._plan = nullptr; }
+    batch_packer(batch_packer&& o) noexcept
+        : _plan(o._plan), _nfields(o._nfields), _rb(o._rb), _offs(std::move(o._offs)) {
+        o._plan = nullptr;
+    }
     batch_packer(batch_packer const&) = delete;
     batch_packer& operator=(batch_packer const&) = delete;
     ~batch_packer() {
@@ -189,6 +220,18 @@ public:
     int unpack(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, void* const* d_cols,
                srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
         return srpc_gpu_unpack(_plan, d_wire, wire_len, n, d_cols, d_status, stream);
+    }
+
+    /// Fixed-size T: n records straight from / into a device copy of a T
+    /// array (the raw bytes of a std::vector<T>, one hipMemcpy), no host
+    /// transpose into columns.  unpack_records writes only the leaf fields.
+    int pack_records(const T* d_records, uint64_t n, uint8_t* d_wire, uint64_t wire_cap,
+                     void* stream = nullptr) const {
+        return srpc_gpu_pack_aos(_plan, d_records, sizeof(T), _offs.data(), n, d_wire, wire_cap, stream);
+    }
+    int unpack_records(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, T* d_records,
+                       srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
+        return srpc_gpu_unpack_aos(_plan, d_wire, wire_len, n, d_records, sizeof(T), _offs.data(), d_status, stream);
     }
 
     /// String schemas: device scratch needed by pack_var / unpack_var for n
@@ -219,11 +262,13 @@ private:
         if (int rc = srpc_plan_create(&d, device, &_plan); rc != SRPC_OK) throw plan_error("srpc_plan_create", rc);
         _nfields = static_cast<uint32_t>(kinds.size());
         srpc_plan_record_bytes(_plan, &_rb);
+        _offs = leaf_offsets<T>();
     }
 
     srpc_plan* _plan = nullptr;
     uint32_t _nfields = 0;
     uint64_t _rb = 0;
+    std::vector<uint32_t> _offs;
 };
 
 }  // namespace srpc::gpu

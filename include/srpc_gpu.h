@@ -166,6 +166,24 @@ int srpc_gpu_unpack(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_
                     uint64_t n, void* const* d_cols, srpc_unpack_status* d_status,
                     void* stream);
 
+/* ---- fixed-size records held as the caller's own structs (AoS) -------------
+ * The reference's caller holds std::vector<T> and loops `p << r`
+ * (packer.hpp:73).  These take the struct array itself, copied to the device
+ * as raw bytes: record r's leaf field f is at d_records + r * record_stride +
+ * field_offsets[f] (host array, nfields entries, T::fields order, nested
+ * messages flattened), naturally aligned (offset, stride and base multiples of
+ * the field size: SRPC_E_ALIGN otherwise).  Wire bytes are those of
+ * srpc_gpu_pack / srpc_gpu_unpack.  unpack_aos writes only the leaf fields'
+ * bytes of each struct; every other byte (padding, a vtable pointer) keeps
+ * what d_records held.  srpc::gpu::batch_packer<T>::pack_records /
+ * unpack_records compute the offsets from T::fields. */
+int srpc_gpu_pack_aos(const srpc_plan* plan, const void* d_records, uint64_t record_stride,
+                      const uint32_t* field_offsets, uint64_t n, uint8_t* d_wire, uint64_t wire_cap,
+                      void* stream);
+int srpc_gpu_unpack_aos(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
+                        void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
+                        srpc_unpack_status* d_status, void* stream);
+
 /* ---- variable-length (string) schemas (SRPC_PATH_VAR) ----------------------
  * A string field f is given as its chars d_cols[f] plus n+1 u64 byte offsets
  * d_str_offs[f] (lengths are offs[i+1]-offs[i]; offs[0] need not be 0).

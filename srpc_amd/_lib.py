@@ -61,6 +61,8 @@ SIGNATURES = {
     "srpc_gather_wire": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, C.c_int, _vp]),
     "srpc_group_gather_wire": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _u64, C.c_int, _vp]),
     "srpc_group_pack_gather": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _u64, C.c_int, _vp]),
+    "srpc_gpu_pack_aos": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, _vp]),
+    "srpc_gpu_unpack_aos": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _u64, _vp, _vp, _vp]),
     "srpc_frames_scratch_bytes": (C.c_int, [_u64, C.c_int, C.POINTER(_u64)]),
     "srpc_frames_classify": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64,
                                        _vp]),

@@ -1,0 +1,223 @@
+// aos.hip -- fixed-size records packed from / unpacked into an array of the
+// caller's own structs (AoS) in device memory.
+//
+// A C++ caller of the reference holds std::vector<T> and packs with
+// `packer p; for (r : recs) p << r;` (packer.hpp:73 -> pack_struct 172-178).
+// Going through SoA columns costs a host-side transpose (host_columns in
+// include/srpc/gpu.hpp: 14 ns per Quad record, 87 ns per multiple_primitives
+// record, profiles/r02_host_columns.log) that dwarfs the GPU pack.  Here the
+// struct array itself is the input: the caller copies the raw bytes of its
+// vector to the device (one DMA) and the kernel reads each leaf field at its
+// byte offset inside T; unpack writes only the leaf fields' bytes into a
+// device copy of the array (everything else -- vtable pointer, padding --
+// stays as the copy brought it), which the caller copies back.
+//
+// Kernels: a workgroup owns a tile of R records (the plan's TILE tiling), one
+// struct per lane: fields straight between the struct array and an LDS image
+// of the tile's wire bytes, which moves to / from HBM in 16-byte pieces with
+// the envelope prefix applied / checked from the plan's periodic template.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "plan.h"
+#include "srpc_gpu.h"
+
+namespace srpc_impl {
+namespace {
+
+struct AosArgs {
+    uint32_t roff[kMaxFields];  // leaf field offset inside the caller's struct
+    uint32_t size[kMaxFields];  // 1, 2, 4 or 8
+    uint32_t woff[kMaxFields];  // offset inside the wire record (prefix included)
+    const uint8_t* period;      // template | mask of one period (prefix_len > 0)
+    uint32_t nfields, wstride, rstride, prefix_len, R, L;
+};
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t load_field(const uint8_t* p, uint32_t sz) {
+    switch (sz) {  // naturally aligned (checked on the host)
+    case 1: return *p;
+    case 2: return *reinterpret_cast<const uint16_t*>(p);
+    case 4: return *reinterpret_cast<const uint32_t*>(p);
+    default: return *reinterpret_cast<const uint64_t*>(p);
+    }
+}
+
+__device__ __forceinline__ void store_field(uint8_t* p, uint64_t v, uint32_t sz) {
+    switch (sz) {
+    case 1: *p = static_cast<uint8_t>(v); break;
+    case 2: *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v); break;
+    case 4: *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(v); break;
+    default: *reinterpret_cast<uint64_t*>(p) = v; break;
+    }
+}
+
+__device__ __forceinline__ void load_period(const AosArgs& a, uint8_t* tmpl) {
+    for (uint32_t i = threadIdx.x; i < (2 * a.L) >> 4; i += kBlock)
+        reinterpret_cast<uint4*>(tmpl)[i] = reinterpret_cast<const uint4*>(a.period)[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_aos(AosArgs a, const uint8_t* __restrict__ recs,
+                                                     uint8_t* __restrict__ wire, uint64_t n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* tmpl = lds + a.R * a.wstride;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) load_period(a, tmpl);
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    // structs -> image, one struct per lane (consecutive lanes, consecutive structs)
+    for (uint32_t e = threadIdx.x; e < nr; e += kBlock) {
+        const uint8_t* src = recs + (rbase + e) * a.rstride;
+        const uint32_t d = e * a.wstride;
+        for (uint32_t f = 0; f < a.nfields; ++f)
+            lds_put_small(lds, d + a.woff[f], load_field(src + a.roff[f], a.size[f]), a.size[f]);
+    }
+    __syncthreads();
+    // image (+ prefix template) -> wire, aligned 16-byte stores
+    uint8_t* dst = wire + rbase * a.wstride;
+    const uint32_t tbytes = nr * a.wstride, full = tbytes >> 4;
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+        uint4 v = reinterpret_cast<const uint4*>(lds)[c];
+        if (a.prefix_len) {
+            const uint32_t ph = (16 * c) % a.L;
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + ph), t = *reinterpret_cast<const uint4*>(tmpl + ph);
+            v = make_uint4((v.x & ~m.x) | t.x, (v.y & ~m.y) | t.y, (v.z & ~m.z) | t.z, (v.w & ~m.w) | t.w);
+        }
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(dst + 16 * c));
+    }
+    if (threadIdx.x == 0)
+        for (uint32_t i = full * 16; i < tbytes; ++i) {
+            const uint32_t ph = i % a.L;
+            dst[i] = a.prefix_len && mask[ph] ? tmpl[ph] : lds[i];
+        }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_aos(AosArgs a, const uint8_t* __restrict__ wire,
+                                                       uint8_t* __restrict__ recs, uint64_t n,
+                                                       srpc_unpack_status* st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* tmpl = lds + a.R * a.wstride;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) load_period(a, tmpl);
+    __syncthreads();
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    const uint8_t* src = wire + rbase * a.wstride;
+    const uint32_t tbytes = nr * a.wstride, full = tbytes >> 4;
+    // wire -> image, every prefix byte checked against the template
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+        const uint4 v = reinterpret_cast<const uint4*>(src)[c];
+        if (a.prefix_len && st) {
+            const uint32_t ph = (16 * c) % a.L;
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + ph), t = *reinterpret_cast<const uint4*>(tmpl + ph);
+            const uint32_t d[4] = {(v.x & m.x) ^ t.x, (v.y & m.y) ^ t.y, (v.z & m.z) ^ t.z, (v.w & m.w) ^ t.w};
+            for (uint32_t w = 0; w < 4; ++w)
+                if (d[w]) {
+                    const uint32_t i = 16 * c + 4 * w + (__builtin_ctz(d[w]) >> 3);
+                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.wstride);
+                    break;
+                }
+        }
+        reinterpret_cast<uint4*>(lds)[c] = v;
+    }
+    if (threadIdx.x == 0)
+        for (uint32_t i = full * 16; i < tbytes; ++i) {
+            const uint8_t b = src[i];
+            const uint32_t ph = i % a.L;
+            if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph]) report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.wstride);
+            lds[i] = b;
+        }
+    __syncthreads();
+    // image -> the leaf fields of the structs (nothing else in them is written)
+    for (uint32_t e = threadIdx.x; e < nr; e += kBlock) {
+        uint8_t* dst = recs + (rbase + e) * a.rstride;
+        const uint32_t s = e * a.wstride;
+        for (uint32_t f = 0; f < a.nfields; ++f) store_field(dst + a.roff[f], lds_u64(lds, s + a.woff[f]), a.size[f]);
+    }
+}
+
+__global__ void k_aos_status(srpc_unpack_status* st, uint32_t flags, uint64_t first_bad) {
+    if (threadIdx.x == 0) {
+        st->flags = flags;
+        st->reserved = 0;
+        st->first_bad_record = first_bad;
+    }
+}
+
+// Validates the layout and fills the kernel arguments.
+int aos_args(const srpc_plan* p, const void* recs, uint64_t stride, const uint32_t* offs, AosArgs* a) {
+    if (!p || p->has_string || !offs || stride == 0 || stride > 0xffffffffull) return SRPC_E_INVALID;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        const uint32_t sz = p->size[f];
+        if (offs[f] + static_cast<uint64_t>(sz) > stride) return SRPC_E_INVALID;
+        if (offs[f] % sz || stride % sz || !aligned(recs, sz)) return SRPC_E_ALIGN;  // natural alignment, as in C++ structs
+        a->roff[f] = offs[f];
+        a->size[f] = sz;
+        a->woff[f] = p->off[f];
+    }
+    a->period = p->d_period;
+    a->nfields = p->nfields;
+    a->wstride = static_cast<uint32_t>(p->stride);
+    a->rstride = static_cast<uint32_t>(stride);
+    a->prefix_len = p->prefix_len;
+    a->L = p->tile_L;
+    return SRPC_OK;
+}
+
+}  // namespace
+}  // namespace srpc_impl
+
+using namespace srpc_impl;
+
+extern "C" {
+
+int srpc_gpu_pack_aos(const srpc_plan* p, const void* d_records, uint64_t record_stride,
+                      const uint32_t* field_offsets, uint64_t n, uint8_t* d_wire, uint64_t wire_cap, void* stream) {
+    const TimedCall timed;
+    AosArgs a{};
+    if (int rc = aos_args(p, d_records, record_stride, field_offsets, &a)) return rc;
+    if (n == 0) return SRPC_OK;
+    if (!d_records || !d_wire) return SRPC_E_INVALID;
+    if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
+    if (!aligned(d_wire, 16)) return SRPC_E_ALIGN;
+    a.R = p->ptile_R;
+    const uint64_t tiles = (n + a.R - 1) / a.R;
+    if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    launch(k_pack_aos, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), static_cast<uint32_t>(p->ptile_lds),
+           static_cast<hipStream_t>(stream), a, static_cast<const uint8_t*>(d_records), d_wire, n);
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
+                        void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
+                        srpc_unpack_status* d_status, void* stream) {
+    const TimedCall timed;
+    AosArgs a{};
+    if (int rc = aos_args(p, d_records, record_stride, field_offsets, &a)) return rc;
+    auto s = static_cast<hipStream_t>(stream);
+    if (d_status) hipLaunchKernelGGL(k_aos_status, dim3(1), dim3(64), 0, s, d_status, 0u, ~0ull);
+    if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    if (!d_records || !d_wire) return SRPC_E_INVALID;
+    if (!aligned(d_wire, 16)) return SRPC_E_ALIGN;
+    uint64_t n_fit = wire_len / p->stride;
+    int ret = SRPC_OK;
+    if (n_fit < n) {  // the records that fit are decoded; the status names the first that does not
+        if (d_status) hipLaunchKernelGGL(k_aos_status, dim3(1), dim3(64), 0, s, d_status, SRPC_STATUS_BOUNDS, n_fit);
+        ret = SRPC_ERR_BOUNDS;
+    } else {
+        n_fit = n;
+    }
+    if (n_fit) {
+        a.R = p->tile_R;
+        const uint64_t tiles = (n_fit + a.R - 1) / a.R;
+        if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_unpack_aos, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), static_cast<uint32_t>(p->tile_lds), s, a,
+               d_wire, static_cast<uint8_t*>(d_records), n_fit, d_status);
+    }
+    return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
+}
+
+}  // extern "C"

@@ -171,6 +171,29 @@ class GpuPacker:
                                                 _dptr(status), _stream(stream)),
                      "srpc_gpu_unpack")
 
+    # -- records as structs (AoS) ---------------------------------------------
+    def _offsets(self, field_offsets: Sequence[int]) -> C.Array:
+        if len(field_offsets) != len(self.schema.kinds):
+            raise ValueError(f"{self.schema.name}: expected {len(self.schema.kinds)} field offsets")
+        return (C.c_uint32 * len(field_offsets))(*[int(o) for o in field_offsets])
+
+    def pack_aos(self, records, record_stride: int, field_offsets: Sequence[int], n: int, wire,
+                 wire_cap: int | None = None, stream=None) -> int:
+        """Pack n records from a device array of structs (e.g. a numpy structured
+        dtype's bytes): field f of record r at r * record_stride + field_offsets[f]."""
+        cap = self.wire_bytes(n) if wire_cap is None else wire_cap
+        check(_lib.lib().srpc_gpu_pack_aos(self._h, _dptr(records), record_stride, self._offsets(field_offsets), n,
+                                           _dptr(wire), cap, _stream(stream)), "srpc_gpu_pack_aos")
+        return self.wire_bytes(n)
+
+    def unpack_aos(self, wire, wire_len: int, n: int, records, record_stride: int, field_offsets: Sequence[int],
+                   status=None, stream=None) -> int:
+        """Unpack n records into the leaf fields of a device array of structs
+        (other bytes untouched).  Returns SRPC_OK or SRPC_ERR_BOUNDS."""
+        return check(_lib.lib().srpc_gpu_unpack_aos(self._h, _dptr(wire), wire_len, n, _dptr(records), record_stride,
+                                                    self._offsets(field_offsets), _dptr(status), _stream(stream)),
+                     "srpc_gpu_unpack_aos")
+
     # -- string schemas (SRPC_PATH_VAR) -------------------------------------
     def var_scratch_bytes(self, n: int, wire_bytes: int) -> int:
         """Device scratch for pack_var (wire_bytes = wire_cap) / unpack_var (= wire_len)."""

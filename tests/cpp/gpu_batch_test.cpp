@@ -89,6 +89,25 @@ static int run(srpc::gpu::batch_packer<T>& bp, size_t n, Fill fill, Eq eq, Emit 
     bool same = out.size() == recs.size();
     for (size_t i = 0; same && i < n; ++i) same = eq(out[i], recs[i]);
     CHECK(same);
+    // the same records straight from / into the raw bytes of the std::vector<T>
+    // (pack_records / unpack_records: no host transpose)
+    T* drecs = nullptr;
+    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&drecs), n * sizeof(T) + 16));
+    HIPCHECK(hipMemcpy(drecs, recs.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemset(dw, 0, want.size()));
+    CHECK(bp.pack_records(drecs, n, dw, want.size()) == SRPC_OK);
+    HIPCHECK(hipMemcpy(got.data(), dw, got.size(), hipMemcpyDeviceToHost));
+    CHECK(got == want);
+    std::vector<T> out2(n);  // default objects: their vtable pointers travel to the device and back
+    HIPCHECK(hipMemcpy(drecs, out2.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    CHECK(bp.unpack_records(dw, want.size(), n, drecs, st) == SRPC_OK);
+    HIPCHECK(hipMemcpy(static_cast<void*>(out2.data()), drecs, n * sizeof(T), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&hs, st, sizeof(hs), hipMemcpyDeviceToHost));
+    CHECK(hs.flags == 0);
+    same = true;
+    for (size_t i = 0; same && i < n; ++i) same = eq(out2[i], recs[i]);
+    CHECK(same);
+    (void)hipFree(drecs);
     for (size_t f = 0; f < hc.col.size(); ++f) { (void)hipFree(dcols[f]); (void)hipFree(dback[f]); }
     (void)hipFree(dw);
     (void)hipFree(st);

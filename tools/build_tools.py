@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 
-TOOLS = {"e2e_square": "e2e_square.hip"}
+TOOLS = {"e2e_square": "e2e_square.hip", "aos_bench": "aos_bench.hip"}
 
 
 def build(name: str = "e2e_square") -> str:
