@@ -82,8 +82,10 @@ typedef enum srpc_kind {
  * Reset by the call itself (stream-ordered) before decoding starts. */
 typedef struct srpc_unpack_status {
     uint32_t flags;             /* OR of SRPC_STATUS_* over the batch          */
-    uint32_t reserved;          /* diagnostics: bit 0 = srpc_gpu_unpack_var_stream
-                                   walked a mis-speculated chunk again        */
+    uint32_t reserved;          /* diagnostics of srpc_gpu_unpack_var_stream: bit 0 =
+                                   a mis-speculated chunk was walked again, bit 1 =
+                                   the parallel repair rounds did not settle every
+                                   chunk and the in-order fixer ran            */
     uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */
 } srpc_unpack_status;
 

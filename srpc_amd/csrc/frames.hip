@@ -17,6 +17,7 @@
 #include <cstring>
 
 #include "plan.h"
+#include "scan.h"
 #include "srpc_gpu.h"
 
 namespace srpc_impl {
@@ -24,7 +25,6 @@ namespace {
 
 constexpr uint32_t kNoClass = SRPC_FRAME_UNKNOWN;
 constexpr int kMaxPlans = SRPC_FRAMES_MAX_PLANS;
-constexpr uint32_t kScanPer = kBlock * 8;  // frames per scan block
 
 struct ClassArgs {
     const uint8_t* prefix[kMaxPlans];  // device prefix of plan k
@@ -82,84 +82,6 @@ __global__ __launch_bounds__(kBlock) void k_classify(ClassArgs a, const uint8_t*
         atomicAdd(reinterpret_cast<unsigned long long*>(&counts[a.nplans + 1]), static_cast<unsigned long long>(__popcll(mu)));
 }
 
-// Exclusive scan of rb[] (u32 response bytes) into out_off[] (u64), 2048 frames
-// per block: block totals, a one-block scan of them, then the apply pass.
-__global__ __launch_bounds__(kBlock) void k_rb_reduce(const uint32_t* __restrict__ rb, uint64_t nf,
-                                                      uint64_t* __restrict__ part) {
-    __shared__ uint64_t ws[kBlock / 64];
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kScanPer;
-    uint64_t s = 0;
-    for (uint32_t j = threadIdx.x; j < kScanPer; j += kBlock)
-        if (base + j < nf) s += rb[base + j];
-    for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-// One block: exclusive scan of the nb block totals in place, thread t owning a
-// contiguous run of them.
-__global__ __launch_bounds__(kBlock) void k_rb_partials(uint64_t* __restrict__ part, uint64_t nb,
-                                                        uint64_t* __restrict__ total) {
-    __shared__ uint64_t ws[kBlock / 64];
-    const uint64_t per = (nb + kBlock - 1) / kBlock;
-    const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
-    uint64_t s = 0;
-    for (uint64_t b = lo; b < hi; ++b) s += part[b];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t inc = s;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t y = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint64_t run = inc - s;
-    for (int w = 0; w < wave; ++w) run += ws[w];
-    for (uint64_t b = lo; b < hi; ++b) {
-        const uint64_t v = part[b];
-        part[b] = run;
-        run += v;
-    }
-    if (threadIdx.x == kBlock - 1) *total = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-__global__ __launch_bounds__(kBlock) void k_rb_apply(const uint32_t* __restrict__ rb, uint64_t nf,
-                                                     const uint64_t* __restrict__ part, const uint64_t* total,
-                                                     uint64_t* __restrict__ out_off) {
-    __shared__ uint64_t v[kScanPer];
-    __shared__ uint64_t ws[kBlock / 64];
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kScanPer;
-    for (uint32_t j = threadIdx.x; j < kScanPer; j += kBlock) v[j] = base + j < nf ? rb[base + j] : 0;
-    __syncthreads();
-    uint64_t loc[8];
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        loc[j] = s;
-        s += v[threadIdx.x * 8 + j];
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t inc = s;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t y = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint64_t before = part[blockIdx.x];
-    for (int w = 0; w < wave; ++w) before += ws[w];
-    before += inc - s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const uint64_t f = base + threadIdx.x * 8 + j;
-        if (f < nf) out_off[f] = before + loc[j];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) out_off[nf] = *total;
-}
-
 // Bucket -> contiguous batch: 4 bytes per lane of the output (n records of
 // rec bytes); record j is frame index[j].
 __global__ __launch_bounds__(kBlock) void k_gather(const uint8_t* __restrict__ buf, const uint32_t* __restrict__ offs,
@@ -208,8 +130,7 @@ extern "C" {
 
 int srpc_frames_scratch_bytes(uint64_t nframes, int nplans, uint64_t* out) {
     if (!out || nplans <= 0 || nplans > kMaxPlans) return SRPC_E_INVALID;
-    const uint64_t nb = (nframes + kScanPer - 1) / kScanPer + 1;
-    *out = 4 * nframes + 8 * nb + 256;
+    *out = 4 * nframes + 8 * xscan_parts(nframes) + 256;
     return SRPC_OK;
 }
 
@@ -241,13 +162,7 @@ int srpc_frames_classify(const srpc_plan* const* req_plans, const uint32_t* resp
         hipLaunchKernelGGL(k_classify, dim3(grid_for(nframes, kBlock)), dim3(kBlock), 0, s, a, d_buf, buf_len, d_offs,
                            nframes, d_class, d_index, d_counts, rb);
     }
-    const uint64_t nb = (nframes + kScanPer - 1) / kScanPer;
-    if (nb) hipLaunchKernelGGL(k_rb_reduce, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s,
-                               static_cast<const uint32_t*>(rb), nframes, part);
-    hipLaunchKernelGGL(k_rb_partials, dim3(1), dim3(kBlock), 0, s, part, nb, d_counts + nplans);
-    hipLaunchKernelGGL(k_rb_apply, dim3(static_cast<uint32_t>(std::max<uint64_t>(nb, 1))), dim3(kBlock), 0, s,
-                       static_cast<const uint32_t*>(rb), nframes, static_cast<const uint64_t*>(part),
-                       static_cast<const uint64_t*>(d_counts + nplans), d_out_off);
+    xscan(static_cast<const uint32_t*>(rb), nframes, part, d_counts + nplans, d_out_off, s);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 

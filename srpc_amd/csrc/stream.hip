@@ -7,24 +7,26 @@
 // record starts is only known once every record before it was read.  Here
 // the record index is found on the device, then the indexed decode runs.
 //
-// 1. k_stream_spec -- the wire is cut into chunks of kChunk bytes, one lane
-//    each.  A lane takes the first position p of its chunk at which kPlaus
+// 1. k_stream_scan / k_stream_walk -- the wire is cut into chunks of kChunk
+//    bytes.  A wave per chunk finds the first position p at which a.plaus
 //    records parse one after another (a plausible record start: a string
 //    length read at a wrong offset is almost always past the end of the
-//    wire) and walks records from there while they start inside the chunk:
-//    record count, the position after them ("exit": the first record start
+//    wire; see k_stream_scan for the one exception), then a lane per chunk
+//    walks records from there while they start inside the chunk: their
+//    starts, count, the position after them ("exit": the first record start
 //    at or past the chunk end, or where a record failed to parse), and why
 //    the walk stopped.
 // 2. k_stream_check -- chunk c is right when its start equals the exit of
 //    chunk c - 1 (or chunk c holds no record start at all), chunk 0 when it
 //    starts at 0.  By induction every chunk up to the first wrong one is
 //    right.
-// 3. k_stream_fix (one workgroup, runs only if a chunk was wrong) -- walks the
-//    chunks from the first wrong one in order, each from its predecessor's
-//    corrected exit, until the stream stops; chunks whose start already
-//    agrees are taken as they are.
+// 3. repair rounds (k_stream_refix / k_stream_recheck, gated) walk the wrong
+//    chunks again from entries that are final; k_stream_fix (one thread,
+//    runs only if chunks are still wrong) walks the chunks from the first
+//    wrong one in order, each from its predecessor's corrected exit, until
+//    the stream stops; chunks whose start already agrees are kept.
 // 4. the chunks' record counts are scanned to record numbers, and
-//    k_stream_index writes rec_offs[] by walking each chunk again;
+//    k_stream_index copies each chunk's record starts into rec_offs[];
 //    k_stream_tail fills what the stream does not hold.
 // The walk is orc_unpack's cursor (oracle/packer_oracle.c): the prefix must
 // match, every read must fit in the wire.  A record that fails stops the
@@ -38,21 +40,29 @@
 #include <cstring>
 
 #include "plan.h"
+#include "scan.h"
 #include "srpc_gpu.h"
 
 namespace srpc_impl {
 namespace {
 
 constexpr uint32_t kChunk = 512;    // wire bytes per speculating lane
-constexpr int kPlaus = 3;           // records that must parse from a candidate start
+// records that must parse from a candidate start: with an envelope prefix of
+// 8 bytes or more a wrong start essentially never matches it, so one; else 2
+// (a wrong start that hops onto a true one passes any count: see k_stream_scan)
+constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint64_t kNone = ~0ull;   // chunk holds no plausible record start
 constexpr uint32_t kStopEnd = 1;    // the walk reached the end of the wire exactly
 constexpr uint32_t kStopBad = 2;    // a record failed to parse at the exit position
+constexpr int kRepairRounds = 3;    // parallel repair rounds before the serial fixer
 
 struct StreamArgs {
     uint32_t size[kMaxFields];  // fixed field bytes, 0 = string
     const uint8_t* prefix;      // device copy (16 zero bytes past the end)
     uint32_t nfields, prefix_len;
+    uint32_t first_len_at;      // byte offset of the first string's u64 length in a record
+    uint32_t plaus;             // records that must parse from a candidate start
+    uint64_t pre8;              // the prefix's first 8 bytes (zero padded)
 };
 
 struct Chunks {      // per chunk (scratch, C entries each)
@@ -62,7 +72,9 @@ struct Chunks {      // per chunk (scratch, C entries each)
     uint32_t* stop;   // kStopEnd / kStopBad / 0
     uint32_t* bad;    // chunk disagrees with its predecessor
     uint32_t* blk;    // per 256 chunks: bit 0 some chunk is bad, bit 1 some chunk stops
-    uint32_t* ctl;    // [0] any bad, [1] the stream's stop chunk, [2] the first bad chunk
+    uint32_t* ctl;    // [0] any bad, [1] the stream's stop chunk, [2] the first bad chunk, [3..6] see below
+    uint64_t* list;   // per chunk: the starts of its records, cap entries each
+    uint32_t cap;     // 1 + kChunk / the smallest record (fixed_bytes): a chunk's records at most
 };
 
 template <typename T>
@@ -121,7 +133,7 @@ __device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, 
 
 // Walk from p while records start before hi: count, exit, stop reason.
 __device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint64_t hi, uint64_t* cnt,
-                     uint64_t* exit, uint32_t* stop) {
+                     uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
     uint64_t k = 0;
     *stop = 0;
     while (p < hi) {
@@ -131,6 +143,7 @@ __device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t
             *stop = kStopBad;
             break;
         }
+        if (k < cap) list[k] = p;  // always: records are >= fixed_bytes long
         ++k;
         p = q;
     }
@@ -139,8 +152,24 @@ __device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t
     *exit = p;
 }
 
+// Necessary for a record to parse at p: the prefix's first (up to 8) bytes
+// match and the first string's length fits the wire.
+__device__ __forceinline__ bool filter(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p) {
+    if (a.first_len_at + 8 > W - p) return false;
+    if (a.prefix_len) {
+        const uint32_t k = a.prefix_len < 8 ? a.prefix_len : 8;
+        const uint64_t mask = k == 8 ? ~0ull : (1ull << (8 * k)) - 1;
+        uint64_t v = 0;
+        if (8 <= W - p) v = ld<uint64_t>(w + p);
+        else
+            for (uint32_t i = 0; i < k; ++i) v |= static_cast<uint64_t>(w[p + i]) << (8 * i);
+        if (((v ^ a.pre8) & mask) != 0) return false;
+    }
+    return ld<uint64_t>(w + p + a.first_len_at) <= W - (p + a.first_len_at + 8);
+}
+
 __device__ __forceinline__ bool plausible(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p) {
-    for (int k = 0; k < kPlaus; ++k) {
+    for (uint32_t k = 0; k < a.plaus; ++k) {
         if (p == W) return k > 0;  // the stream may end right after a record
         uint32_t err;
         const uint64_t q = parse_at(a, w, W, p, &err);
@@ -150,29 +179,78 @@ __device__ __forceinline__ bool plausible(const StreamArgs& a, const uint8_t* w,
     return true;
 }
 
-// Chunk c's speculation: its first plausible record start, the records from
-// there that start inside the chunk, and the position after them.  A chunk
-// with no plausible start (inside a long record) passes its entry through:
-// start = exit = kNone, no records.
-__global__ __launch_bounds__(kBlock) void k_stream_spec(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+// Chunk c's speculation, in two kernels.  k_stream_scan (a wave per chunk,
+// its lanes on 64 consecutive candidate positions, so the loads coalesce):
+// the chunk's first plausible record start.  A start 1-3 bytes early is
+// plausible too: its first string length reads the previous record's last
+// chars as low bytes and the true length (little-endian, small) shifted up,
+// and the jump it makes lands on a true record start about once per average
+// record size -- after which every record parses.  So of the plausible starts
+// within the 8 bytes of a length field the one with the smallest first string
+// length is taken: the true start (random strings: 6 % of chunks wrong
+// without this, ~0.05 % with it).  A chunk with no plausible start (inside a
+// long record) passes its entry through: start = exit = kNone, no records.
+__global__ __launch_bounds__(kBlock) void k_stream_scan(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
                                                         uint64_t C, Chunks ch) {
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= C) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    if (c >= C) return;  // wave-uniform
     const uint64_t lo = c * kChunk, hi = min(lo + kChunk, W);
     uint64_t b = kNone;
     if (c == 0) {
         b = 0;  // the stream starts at 0: no speculation
     } else {
-        for (uint64_t p = lo; p < hi; ++p)
-            if (plausible(a, w, W, p)) {
-                b = p;
+        // a cheap filter at all 512 positions first (the loads of the 8
+        // windows issued together): the prefix's first bytes and the first
+        // string's length; only positions that pass parse whole records
+        uint32_t pass = 0;
+#pragma unroll
+        for (int k = 0; k < static_cast<int>(kChunk / 64); ++k) {
+            const uint64_t p = lo + 64 * k + lane;
+            if (p < hi && filter(a, w, W, p)) pass |= 1u << k;
+        }
+        for (int k = 0; k < static_cast<int>(kChunk / 64); ++k) {
+            const uint64_t p = lo + 64 * k + lane;
+            const uint64_t m = __ballot(((pass >> k) & 1) && plausible(a, w, W, p));
+            if (m) {
+                b = lo + 64 * k + __builtin_ctzll(m);
                 break;
             }
+        }
+        if (b != kNone) {
+            // candidates b .. b + 7: argmin of (first string length, position)
+            const uint64_t q = b + lane;
+            bool cand = lane < 8 && q < hi && a.first_len_at + 8 <= W - q;
+            uint64_t l = cand ? ld<uint64_t>(w + q + a.first_len_at) : ~0ull;
+            if (cand && lane > 0 && !plausible(a, w, W, q)) cand = false;
+            uint64_t kl = cand ? l : ~0ull;
+            uint32_t ki = cand ? lane : 64u;
+            for (int d = 32; d > 0; d >>= 1) {
+                const uint64_t ol = __shfl_xor(kl, d, 64);
+                const uint32_t oi = __shfl_xor(ki, d, 64);
+                if (ol < kl || (ol == kl && oi < ki)) {
+                    kl = ol;
+                    ki = oi;
+                }
+            }
+            b += ki;  // lane 0 (b itself) is always a candidate
+        }
     }
+    if (lane == 0) ch.start[c] = b;
+}
+
+// k_stream_walk (a lane per chunk): the records from the chunk's start that
+// start inside the chunk -- their starts, count, the position after them and
+// why the walk stopped.
+__global__ __launch_bounds__(kBlock) void k_stream_walk(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+                                                        uint64_t C, Chunks ch) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t hi = min((c + 1) * kChunk, W);
+    const uint64_t b = ch.start[c];
     uint64_t cnt = 0, exit = kNone;
     uint32_t stop = 0;
-    if (b != kNone) walk(a, w, W, b, hi, &cnt, &exit, &stop);
-    ch.start[c] = b;
+    if (b != kNone) walk(a, w, W, b, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
     ch.cnt[c] = cnt;
     ch.exit[c] = exit;
     ch.stop[c] = stop;
@@ -197,10 +275,25 @@ __device__ __forceinline__ bool agrees(uint64_t e, uint64_t chunk_hi, uint64_t s
     return e >= chunk_hi ? start == kNone : start == e;
 }
 
+// A wave's bad chunks: one atomic per wave on the flags (every lane of the
+// wave calls this: thousands of bad chunks on one control word serialised the
+// check kernel), one per 256-chunk block word.
+__device__ __forceinline__ void note_bad(const Chunks& ch, uint64_t c, bool bad, int any_at, int first_at) {
+    const uint64_t m = __ballot(bad);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+    if (lane == lead) {  // the wave's first bad chunk; a wave's 64 chunks share one block word
+        atomicOr(&ch.ctl[any_at], 1u);
+        atomicMin(&ch.ctl[first_at], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
+        atomicOr(&ch.blk[c >> 8], 1u);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_stream_check(uint64_t W, uint64_t C, Chunks ch) {
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c == 0 && C) ch.bad[0] = 0;
     if (c >= C || c == 0) {
-        if (c == 0 && c < C) ch.bad[0] = 0;
+        note_bad(ch, c, false, 0, 2);
         return;
     }
     const uint64_t hi = min((c + 1) * kChunk, W);
@@ -209,14 +302,69 @@ __global__ __launch_bounds__(kBlock) void k_stream_check(uint64_t W, uint64_t C,
     // after a stop nothing counts (masked later); otherwise start must agree
     const bool ok = stopped || agrees(e, hi, ch.start[c]);
     ch.bad[c] = ok ? 0u : 1u;
-    if (!ok) {
-        atomicOr(&ch.blk[c >> 8], 1u);
-        atomicOr(&ch.ctl[0], 1u);
-        atomicMin(&ch.ctl[2], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
-    }
+    note_bad(ch, c, !ok, 0, 2);
 }
 
-// The stream's stop among the chunks before the first bad one (all right).
+// Parallel repair rounds (before the serial fixer): every bad chunk walks
+// again from its entry as it stands, then every chunk is checked again.  The
+// first bad chunk's entry is final, so each round repairs at least it, and
+// isolated mis-speculations (the common case: a start one byte early whose
+// u64 length reads as len * 256 + a char, ~1 % of chunks on random strings)
+// all in one round.  ctl[3] / ctl[4]: the recheck's any-bad / first-bad.
+__global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+                                                         uint64_t C, Chunks ch) {
+    if (ch.ctl[0] == 0) return;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C || !ch.bad[c]) return;
+    // only a chunk whose entry is final: no bad chunk between it and the chunk
+    // that provides its entry (a chunk marked bad only because its
+    // predecessor was wrong keeps its own, probably right, speculation)
+    for (uint64_t j = c; j-- > 0;) {
+        if (ch.bad[j]) return;
+        if (ch.start[j] != kNone) break;
+    }
+    const uint64_t hi = min((c + 1) * kChunk, W);
+    bool stopped;
+    const uint64_t e = entry_of(ch, c, &stopped);
+    if (stopped) return;
+    uint64_t cnt = 0, exit = kNone, start = kNone;
+    uint32_t stop = 0;
+    if (e < hi) {
+        start = e;
+        walk(a, w, W, e, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
+    }
+    ch.start[c] = start;
+    ch.cnt[c] = cnt;
+    ch.exit[c] = exit;
+    ch.stop[c] = stop;
+    if (stop) atomicOr(&ch.blk[c >> 8], 2u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t C, Chunks ch) {
+    if (ch.ctl[0] == 0) return;
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (c >= C || c == 0) {
+        note_bad(ch, c, false, 3, 4);
+        return;
+    }
+    const uint64_t hi = min((c + 1) * kChunk, W);
+    bool stopped;
+    const uint64_t e = entry_of(ch, c, &stopped);
+    const bool ok = stopped || agrees(e, hi, ch.start[c]);
+    ch.bad[c] = ok ? 0u : 1u;
+    note_bad(ch, c, !ok, 3, 4);
+}
+
+__global__ void k_stream_round_end(Chunks ch) {
+    if (threadIdx.x != 0 || ch.ctl[0] == 0) return;
+    ch.ctl[0] = ch.ctl[3];
+    ch.ctl[2] = ch.ctl[4];
+    ch.ctl[3] = 0;
+    ch.ctl[4] = 0xffffffffu;
+    ch.ctl[5] += 1;  // rounds that found something to repair (diagnostic)
+}
+
+// The stream's stop among the chunks before the first bad one (all right).// The stream's stop among the chunks before the first bad one (all right).
 __global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c < C && c < ch.ctl[2] && ch.stop[c] && ch.start[c] != kNone)
@@ -229,6 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
 // are kept; 256-chunk blocks with no bad chunk and no stop are skipped.
 __global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W, uint64_t C, Chunks ch) {
     if (threadIdx.x != 0 || ch.ctl[0] == 0 || ch.ctl[1] < ch.ctl[2]) return;
+    ch.ctl[6] = 1;
     uint64_t c = ch.ctl[2];
     while (c < C) {
         const uint64_t hi = min((c + 1) * kChunk, W);
@@ -243,7 +392,7 @@ __global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64
             uint32_t stop = 0;
             if (e < hi) {
                 start = e;
-                walk(a, w, W, e, hi, &cnt, &exit, &stop);
+                walk(a, w, W, e, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
             }
             ch.start[c] = start;
             ch.cnt[c] = cnt;
@@ -268,21 +417,18 @@ __global__ __launch_bounds__(kBlock) void k_stream_mask(uint64_t C, Chunks ch, u
     if (c < C) counts[c] = c > ch.ctl[1] ? 0 : ch.cnt[c];
 }
 
-// rec_offs[recbase[c] + k] for the chunk's records (k-th start), up to index n.
-__global__ __launch_bounds__(kBlock) void k_stream_index(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
-                                                         uint64_t C, Chunks ch, const uint64_t* __restrict__ counts,
+// rec_offs[recbase[c] + k] = the chunk's k-th record start, up to index n
+// (a lane per chunk, from the starts its walk kept).
+__global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, const uint64_t* __restrict__ counts,
                                                          const uint64_t* __restrict__ recbase, uint64_t n,
                                                          uint64_t* __restrict__ rec_offs) {
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (c >= C || counts[c] == 0) return;
-    uint64_t r = recbase[c];
-    if (r > n) return;
-    uint64_t p = ch.start[c];
-    for (uint64_t k = 0; k < counts[c] && r <= n; ++k, ++r) {  // [n]: the start of record n, if any
-        rec_offs[r] = p;
-        uint32_t err;
-        p = parse_at(a, w, W, p, &err);
-    }
+    const uint64_t r0 = recbase[c];
+    if (r0 > n) return;
+    const uint64_t* list = ch.list + c * ch.cap;
+    const uint64_t k1 = min<uint64_t>(counts[c], n - r0 + 1);  // [n]: the start of record n, if any
+    for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = list[k];
 }
 
 // Records the stream holds: T = sum of counts.  rec_offs[T] = where the stream
@@ -305,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_tail(uint64_t W, uint64_t C, 
 // Diagnostic (srpc_unpack_status.reserved bit 0): some speculated chunk had
 // to be walked again.
 __global__ void k_stream_note(const Chunks ch, srpc_unpack_status* st) {
-    if (threadIdx.x == 0 && ch.ctl[0]) atomicOr(&st->reserved, 1u);
+    if (threadIdx.x == 0 && (ch.ctl[5] || ch.ctl[6])) atomicOr(&st->reserved, 1u | (ch.ctl[6] ? 2u : 0u));
 }
 
 __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
@@ -313,6 +459,10 @@ __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
         ch.ctl[0] = 0;            // some chunk is bad
         ch.ctl[1] = 0xffffffffu;  // the chunk where the stream stops
         ch.ctl[2] = 0xffffffffu;  // the first bad chunk
+        ch.ctl[3] = 0;            // repair round: any bad
+        ch.ctl[4] = 0xffffffffu;  // repair round: first bad
+        ch.ctl[5] = 0;            // repair rounds run
+        ch.ctl[6] = 0;            // the serial fixer ran
     }
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nblk;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
@@ -322,10 +472,10 @@ __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct StreamLayout {
-    uint64_t C, start, cnt, exit, counts, recbase, stop, bad, blk, ctl, total;
+    uint64_t C, start, cnt, exit, counts, recbase, stop, bad, blk, ctl, parts, list, cap, total;
 };
 
-StreamLayout stream_layout(uint64_t wire_len) {
+StreamLayout stream_layout(uint64_t wire_len, uint32_t fixed_bytes) {
     StreamLayout L{};
     L.C = std::max<uint64_t>(1, (wire_len + kChunk - 1) / kChunk);
     uint64_t o = 0;
@@ -347,42 +497,13 @@ StreamLayout stream_layout(uint64_t wire_len) {
     o += r256(4 * ((L.C + 255) / 256));
     L.ctl = o;
     o += 256;
+    L.parts = o;  // the chunk-count scan's block totals, then its total
+    o += r256(8 * (xscan_parts(L.C) + 1));
+    L.cap = 1 + kChunk / std::max<uint32_t>(fixed_bytes, 1);
+    L.list = o;
+    o += r256(8 * L.C * L.cap);
     L.total = o;
     return L;
-}
-
-// Device scan of counts[0..C) into recbase[0..C] (exclusive, [C] = total),
-// one workgroup per 2048 values + a partials pass (C is small: wire / 512).
-__global__ __launch_bounds__(kBlock) void k_small_scan(const uint64_t* __restrict__ v, uint64_t C,
-                                                       uint64_t* __restrict__ out) {
-    // a single workgroup walks the array in 256-value steps with a running total
-    __shared__ uint64_t wsum[kBlock / 64];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint64_t base = 0; base < C; base += kBlock) {
-        const uint64_t i = base + threadIdx.x;
-        const uint64_t x = i < C ? v[i] : 0;
-        uint64_t inc = x;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += y;
-        }
-        if (lane == 63) wsum[wave] = inc;
-        __syncthreads();
-        uint64_t before = carry, all = 0;
-        for (int k = 0; k < kBlock / 64; ++k) {
-            before += k < wave ? wsum[k] : 0;
-            all += wsum[k];
-        }
-        if (i < C) out[i] = before + inc - x;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += all;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[C] = carry;
 }
 
 }  // namespace
@@ -396,7 +517,7 @@ int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t 
     if (!p || !out || !p->has_string) return SRPC_E_INVALID;
     uint64_t var = 0;
     if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
-    *out = r256(var) + stream_layout(wire_len).total;
+    *out = r256(var) + stream_layout(wire_len, p->fixed_bytes).total;
     return SRPC_OK;
 }
 
@@ -412,11 +533,12 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     srpc_plan_var_scratch_bytes(p, n, wire_len, &var);
     auto s = static_cast<hipStream_t>(stream);
     auto* base = static_cast<uint8_t*>(scratch) + r256(var);
-    const StreamLayout L = stream_layout(wire_len);
+    const StreamLayout L = stream_layout(wire_len, p->fixed_bytes);
     Chunks ch{reinterpret_cast<uint64_t*>(base + L.start), reinterpret_cast<uint64_t*>(base + L.cnt),
               reinterpret_cast<uint64_t*>(base + L.exit),  reinterpret_cast<uint32_t*>(base + L.stop),
               reinterpret_cast<uint32_t*>(base + L.bad),   reinterpret_cast<uint32_t*>(base + L.blk),
-              reinterpret_cast<uint32_t*>(base + L.ctl)};
+              reinterpret_cast<uint32_t*>(base + L.ctl),   reinterpret_cast<uint64_t*>(base + L.list),
+              static_cast<uint32_t>(L.cap)};
     auto* counts = reinterpret_cast<uint64_t*>(base + L.counts);
     auto* recbase = reinterpret_cast<uint64_t*>(base + L.recbase);
     StreamArgs a{};
@@ -424,6 +546,10 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     a.prefix = p->d_prefix;
     a.nfields = p->nfields;
     a.prefix_len = p->prefix_len;
+    a.first_len_at = p->prefix_len;
+    for (uint32_t f = 0; f < p->nfields && p->size[f]; ++f) a.first_len_at += p->size[f];
+    a.plaus = p->prefix_len >= 8 ? kPlausPrefixed : kPlausBare;
+    for (uint32_t i = 0; i < 8 && i < p->prefix_len; ++i) a.pre8 |= static_cast<uint64_t>(p->h_prefix[i]) << (8 * i);
     const uint64_t C = L.C;
     const uint64_t g = (C + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
@@ -432,18 +558,26 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     launch(k_stream_ctl_reset, dim3(static_cast<uint32_t>(std::min<uint64_t>((nblk + 255) / 256 + 1, 1024))),
            dim3(256), 0, s, ch, nblk);
     if (wire_len) {
-        launch(k_stream_spec, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+        const uint64_t gw = (C + kBlock / 64 - 1) / (kBlock / 64);
+        if (gw > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_stream_scan, dim3(static_cast<uint32_t>(gw)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+        launch(k_stream_walk, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
         launch(k_stream_check, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
+        for (int r = 0; r < kRepairRounds; ++r) {  // gated: no-ops once every chunk agrees
+            launch(k_stream_refix, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+            launch(k_stream_recheck, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
+            launch(k_stream_round_end, dim3(1), dim3(64), 0, s, ch);
+        }
         launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
         launch(k_stream_fix, dim3(1), dim3(64), 0, s, a, wire, wire_len, C, ch);
         launch(k_stream_mask, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch, counts);
     } else {
         launch(k_stream_mask, dim3(1), dim3(kBlock), 0, s, 0ull, ch, counts);
     }
-    launch(k_small_scan, dim3(1), dim3(kBlock), 0, s, static_cast<const uint64_t*>(counts), wire_len ? C : 0ull,
-           recbase);
+    auto* parts = reinterpret_cast<uint64_t*>(base + L.parts);
+    xscan(static_cast<const uint64_t*>(counts), wire_len ? C : 0ull, parts, parts + xscan_parts(C), recbase, s);
     if (wire_len)
-        launch(k_stream_index, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch,
+        launch(k_stream_index, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch,
                static_cast<const uint64_t*>(counts), static_cast<const uint64_t*>(recbase), n, rec_offs);
     launch(k_stream_tail, dim3(static_cast<uint32_t>(std::min<uint64_t>(n / kBlock + 1, 4096))), dim3(kBlock), 0, s,
            wire_len, wire_len ? C : 0ull, ch, static_cast<const uint64_t*>(recbase), n, rec_offs);

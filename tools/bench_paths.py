@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--var-kernel", default="", help="VAR cases: comma list of pack kernels to time "
                     "(1 record tiles, 0 scan + walk; default: the plan's default)")
     ap.add_argument("--var-caps", default="", help="VAR record tiles: IMAGE:CHARS bytes (default: the plan's)")
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="VAR cases: skip the index-free stream decode timing")
     args = ap.parse_args()
 
     import numpy as np
@@ -93,6 +95,41 @@ def main():
                      "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
                      "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
 
+    def aos_case(name, sch, n):
+        """Records as C-aligned structs behind an 8-byte vtable slot (a C++
+        std::vector<T> copied to the device): srpc_gpu_pack_aos / unpack_aos.
+        Algorithmic bytes: the whole struct array (read by pack, written by
+        unpack) + the wire."""
+        if args.only not in name:
+            return
+        p = GpuPacker(sch)
+        fmts = [np.uint64] + [np.dtype(oracle.KIND_DTYPE[k]) for k in sch.kinds]
+        dt = np.dtype({"names": ["_v"] + [f"f{i}" for i in range(len(sch.kinds))], "formats": fmts}, align=True)
+        rng = np.random.default_rng(3)
+        recs = rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt)
+        for i, k in enumerate(sch.kinds):
+            if k == oracle.BOOL:
+                recs[f"f{i}"] &= 1
+        offs = [dt.fields[f"f{i}"][1] for i in range(len(sch.kinds))]
+        drecs = t_u8(recs)
+        back = torch.empty_like(drecs)
+        wire = torch.empty(n * p.record_bytes + 16, dtype=torch.uint8, device=dev)
+        p.pack_aos(drecs, dt.itemsize, offs, n, wire, stream=s)
+        torch.cuda.synchronize()
+        m = 4096
+        ok = wire[: m * p.record_bytes].cpu().numpy().tobytes() == oracle.pack(
+            sch.kinds, [np.ascontiguousarray(recs[f"f{i}"][:m]) for i in range(len(sch.kinds))], m)
+        alg = n * dt.itemsize + n * p.record_bytes
+        tp = timeit(lambda: p.pack_aos(drecs, dt.itemsize, offs, n, wire, stream=s))
+        back.copy_(drecs)
+        tu = timeit(lambda: p.unpack_aos(wire, n * p.record_bytes, n, back, dt.itemsize, offs, stream=s))
+        ok = ok and torch.equal(back, drecs)
+        rows.append({"case": name, "path": "aos", "records": n, "record_bytes": p.record_bytes,
+                     "struct_bytes": dt.itemsize, "alg_bytes": alg, "pack_us": round(tp * 1e6, 2),
+                     "unpack_us": round(tu * 1e6, 2), "pack_GBps": round(alg / tp / 1e9, 1),
+                     "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
+                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
+
     def var_case(name, kinds, n, maxlen, prefix=b""):
         if args.only not in name:
             return
@@ -141,11 +178,24 @@ def main():
             ok = wire[:total].cpu().numpy().tobytes() == want
             tp = timeit(lambda: p.pack_var(dcols, doffs, n, wire, total, rec, scratch, sb, stream=s))
             tu = timeit(lambda: p.unpack_var(wire, total, n, rec, outs, ooffs, scratch, sb, stream=s))
-            rows.append({"case": label, "path": "var", "records": n, "wire_bytes": total, "alg_bytes": alg,
-                         "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
-                         "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
-                         "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
-                         "parity_ok": bool(ok)})
+            row = {"case": label, "path": "var", "records": n, "wire_bytes": total, "alg_bytes": alg,
+                   "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
+                   "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
+                   "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
+                   "parity_ok": bool(ok)}
+            if args.stream:
+                # the same wire decoded with NO record index (srpc_gpu_unpack_var_stream),
+                # the index rebuilt on the device and written out (8 B per record more)
+                ssb = p.var_stream_scratch_bytes(n, total)
+                sscr = torch.empty(ssb + 256, dtype=torch.uint8, device=dev)
+                sbase = sscr.data_ptr() + (-sscr.data_ptr()) % 256
+                rec2 = torch.empty(8 * (n + 1), dtype=torch.uint8, device=dev)
+                ts = timeit(lambda: p.unpack_var_stream(wire, total, n, rec2, outs, ooffs, sbase, ssb, stream=s))
+                torch.cuda.synchronize()
+                row["parity_ok"] = row["parity_ok"] and torch.equal(rec2, rec)
+                salg = alg + 8 * (n + 1)
+                row.update({"stream_us": round(ts * 1e6, 2), "stream_frac": round(salg / ts / 8e12, 4)})
+            rows.append(row)
 
     N = 1 << 24
     fixed_case("quad_dword_16M", QUAD, N)
@@ -155,6 +205,9 @@ def main():
                                               ("d", "int16"), ("e", "int32"), ("f", "int64")), N)
     fixed_case("square_request_53B_16M", NUMBER, N, srpc_amd.request_prefix(SQUARE_METHOD, "Number"))
     fixed_case("square_response_19B_16M", NUMBER, N, srpc_amd.response_prefix(0, "Number"))
+    aos_case("quad_aos_16M", QUAD, N)
+    aos_case("all_kinds_aos_16M", Schema.of("all_kinds", ("a", "bool"), ("b", "int8"), ("c", "char"),
+                                            ("d", "int16"), ("e", "int32"), ("f", "int64")), N)
     var_case("multiple_primitives_str0-64_4M", [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING],
              1 << 22, 64)
     var_case("string_0-1024_1M", [oracle.STRING], 1 << 20, 1024)
@@ -168,9 +221,10 @@ def main():
         with open(args.out, "w") as f:
             f.write(txt)
     for r in rows:
+        extra = f'  stream {r["stream_us"]:8.1f} us ({r["stream_frac"]:.3f})' if "stream_us" in r else ""
         print(f'{r["case"]:34s} {r["path"]:5s} pack {r["pack_us"]:9.1f} us {r["pack_GBps"]:7.1f} GB/s '
               f'({r["pack_frac"]:.3f})  unpack {r["unpack_us"]:9.1f} us {r["unpack_GBps"]:7.1f} GB/s '
-              f'({r["unpack_frac"]:.3f})  parity={r["parity_ok"]}')
+              f'({r["unpack_frac"]:.3f})  parity={r["parity_ok"]}{extra}')
 
 
 if __name__ == "__main__":
