@@ -31,6 +31,8 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -106,6 +108,8 @@ struct batch_stats {
     uint64_t h2d_bytes = 0;
     uint64_t d2h_bytes = 0;
     double gpu_seconds = 0;  // H2D + classify + unpack + handler + pack + D2H, host-timed per batch
+    double classify_seconds = 0;     // of which: H2D + classify + the counts' D2H (first sync)
+    double first_batch_seconds = 0;  // gpu_seconds of the connection's first batch
     double recv_seconds = 0;
     double send_seconds = 0;
     double fallback_seconds = 0;
@@ -159,9 +163,15 @@ public:
         m->fin = m->in->record_bytes();
         m->fout = m->out->record_bytes();
         Req rq{};
-        for_each_leaf<Req>(rq, [&](const auto& v) { m->req_cols.push_back(alloc(_max * sizeof(v) + 16)); });
+        for_each_leaf<Req>(rq, [&](const auto& v) {
+            m->req_bytes.push_back(_max * sizeof(v) + 16);
+            m->req_cols.push_back(alloc(m->req_bytes.back()));
+        });
         Resp rs{};
-        for_each_leaf<Resp>(rs, [&](const auto& v) { m->resp_cols.push_back(alloc(_max * sizeof(v) + 16)); });
+        for_each_leaf<Resp>(rs, [&](const auto& v) {
+            m->resp_bytes.push_back(_max * sizeof(v) + 16);
+            m->resp_cols.push_back(alloc(m->resp_bytes.back()));
+        });
         _m.push_back(std::move(m));
         release();  // buffers are sized for the largest frames on the next serve
     }
@@ -206,6 +216,10 @@ public:
             }
             const bool oversize = next_hdr && next_len > cap;
             const bool full = nf == _max || have == cap || oversize;
+            if (_trace)
+                std::fprintf(stderr, "recv: have %llu walked %llu nf %llu next %llu%s%s\n", (unsigned long long)have,
+                             (unsigned long long)walked, (unsigned long long)nf, (unsigned long long)next_len,
+                             eof ? " eof" : "", full ? " full" : "");
             if (nf == 0 && !oversize) {
                 if (eof) break;
                 continue;
@@ -232,7 +246,11 @@ private:
         std::unique_ptr<raw_plan> in, out;
         uint64_t fin = 0, fout = 0;
         std::vector<void*> req_cols, resp_cols;
+        std::vector<uint64_t> req_bytes, resp_bytes;
     };
+    void memset_cols(std::vector<void*> const& cols, std::vector<uint64_t> const& bytes) {
+        for (size_t f = 0; f < cols.size(); ++f) check(hipMemsetAsync(cols[f], 0, bytes[f], _s));
+    }
 
     static double secs(clock::time_point t0) { return std::chrono::duration<double>(clock::now() - t0).count(); }
     static void check(hipError_t e) {
@@ -294,6 +312,69 @@ private:
             _in_plans.push_back(m->in->get());
             _resp_bytes.push_back(static_cast<uint32_t>(m->fout));
         }
+        warm_up();
+    }
+
+    /// One-frame run of every kernel the batches use (the library's and each
+    /// handler, on one all-zero record) and one copy through every staging
+    /// buffer, at serve start: first uses cost milliseconds that otherwise land
+    /// on the connection's first batch (profiles/r02_e2e_warmup.log).
+    void warm_up() {
+        const int K = static_cast<int>(_m.size());
+        const uint64_t out_cap = _max * max_fout();
+        check(hipMemsetAsync(_d_out, 0, out_cap + 16, _s));
+        check(hipMemsetAsync(_d_resp, 0, out_cap + 16, _s));
+        check(hipMemsetAsync(_d_gather, 0, _cap + 16, _s));
+        check(hipMemsetAsync(_d_index, 0, 4 * _m.size() * _max + 16, _s));
+        check(hipMemsetAsync(_d_out_off, 0, 8 * (_max + 1) + 16, _s));
+        check(hipMemsetAsync(_d_cls, 0, _max + 16, _s));
+        check(hipMemsetAsync(_d_scratch, 0, _scratch_bytes, _s));
+        for (auto const& m : _m) {
+            memset_cols(m->req_cols, m->req_bytes);
+            memset_cols(m->resp_cols, m->resp_bytes);
+        }
+        std::memset(_h_in, 0, _cap);
+        std::memset(_h_offs, 0, 4 * _max);
+        // a batch's exact sequence of copies and launches on one all-zero frame,
+        // twice (the first pass pays the first uses; whole buffers move)
+        for (int pass = 0; pass < 2; ++pass) {
+            check(hipMemcpyAsync(_d_in, _h_in, _cap, hipMemcpyHostToDevice, _s));
+            check(hipMemcpyAsync(_d_offs, _h_offs, 4 * _max, hipMemcpyHostToDevice, _s));
+            check_srpc(srpc_frames_classify(_in_plans.data(), _resp_bytes.data(), K, static_cast<const uint8_t*>(_d_in),
+                                            8, static_cast<const uint32_t*>(_d_offs), 1, static_cast<uint8_t*>(_d_cls),
+                                            static_cast<uint32_t*>(_d_index), static_cast<uint64_t*>(_d_counts),
+                                            static_cast<uint64_t*>(_d_out_off), _d_scratch, _scratch_bytes, _s),
+                       "srpc_frames_classify");
+            check(hipMemcpyAsync(_h_counts, _d_counts, 8 * (K + 2), hipMemcpyDeviceToHost, _s));
+            check(hipStreamSynchronize(_s));
+            check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
+            for (auto const& m : _m) {
+                check_srpc(srpc_frames_gather(static_cast<const uint8_t*>(_d_in), static_cast<const uint32_t*>(_d_offs),
+                                              static_cast<const uint32_t*>(_d_index), 1, static_cast<uint32_t>(m->fin),
+                                              static_cast<uint8_t*>(_d_gather), _s),
+                           "srpc_frames_gather");
+                (void)srpc_gpu_unpack(m->in->get(), static_cast<const uint8_t*>(_d_gather), m->fin, 1,
+                                      m->req_cols.data(), _d_status, _s);  // a prefix error on the zero frame: expected
+                // the handler's own kernels load their code object on first use
+                // too: it runs on the one zero record (its output is never sent)
+                check_srpc(m->handler(m->req_cols.data(), m->resp_cols.data(), 1, _s), "batch handler (warm-up)");
+                check_srpc(srpc_gpu_pack(m->out->get(), m->resp_cols.data(), 1, static_cast<uint8_t*>(_d_out), m->fout,
+                                         _s),
+                           "srpc_gpu_pack");
+                check_srpc(srpc_gpu_pack(m->out->get(), m->resp_cols.data(), 1, static_cast<uint8_t*>(_d_resp), m->fout,
+                                         _s),
+                           "srpc_gpu_pack");
+                check_srpc(srpc_frames_scatter(static_cast<const uint8_t*>(_d_resp),
+                                               static_cast<const uint32_t*>(_d_index), 1, static_cast<uint32_t>(m->fout),
+                                               static_cast<const uint64_t*>(_d_out_off), static_cast<uint8_t*>(_d_out),
+                                               _s),
+                           "srpc_frames_scatter");
+            }
+            check(hipMemcpyAsync(_h_out, _d_out, out_cap, hipMemcpyDeviceToHost, _s));
+            check(hipMemcpyAsync(_h_cls, _d_cls, _max, hipMemcpyDeviceToHost, _s));
+            check(hipMemcpyAsync(_h_status, _d_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
+            check(hipStreamSynchronize(_s));
+        }
     }
     void release() {
         for (void* p : {_d_in, _d_offs, _d_cls, _d_index, _d_counts, _d_out_off, _d_gather, _d_resp, _d_out,
@@ -314,6 +395,10 @@ private:
     /// The GPU path for the nf whole frames in _h_in[0, used).
     void process(int fd, uint64_t nf, uint64_t used, batch_stats& st) {
         auto t0 = clock::now();
+        auto mark = [&](const char* what) {
+            if (_trace) std::fprintf(stderr, "batch %llu nf %llu %-10s %.3f ms\n", (unsigned long long)st.gpu_batches,
+                                    (unsigned long long)nf, what, 1e3 * secs(t0));
+        };
         const int K = static_cast<int>(_m.size());
         auto* d_in = static_cast<uint8_t*>(_d_in);
         auto* d_offs = static_cast<uint32_t*>(_d_offs);
@@ -322,12 +407,16 @@ private:
         auto* d_out_off = static_cast<uint64_t*>(_d_out_off);
         check(hipMemcpyAsync(d_in, _h_in, used, hipMemcpyHostToDevice, _s));
         check(hipMemcpyAsync(d_offs, _h_offs, 4 * nf, hipMemcpyHostToDevice, _s));
+        mark("h2d");
         check_srpc(srpc_frames_classify(_in_plans.data(), _resp_bytes.data(), K, d_in, used, d_offs, nf,
                                         static_cast<uint8_t*>(_d_cls), d_idx, d_counts, d_out_off, _d_scratch,
                                         _scratch_bytes, _s),
                    "srpc_frames_classify");
         check(hipMemcpyAsync(_h_counts, d_counts, 8 * (K + 2), hipMemcpyDeviceToHost, _s));
+        mark("classify");
         check(hipStreamSynchronize(_s));
+        mark("sync1");
+        st.classify_seconds += secs(t0);
         const uint64_t total = _h_counts[K], unknown = _h_counts[K + 1];
         bool mixed = false;
         check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
@@ -346,9 +435,12 @@ private:
             }
             check_srpc(srpc_gpu_unpack(m.in->get(), src, n * m.fin, n, m.req_cols.data(), _d_status, _s),
                        "srpc_gpu_unpack");
+            mark("unpack");
             check_srpc(m.handler(m.req_cols.data(), m.resp_cols.data(), n, _s), "batch handler");
+            mark("handler");
             auto* dst = static_cast<uint8_t*>(whole ? _d_out : _d_resp);
             check_srpc(srpc_gpu_pack(m.out->get(), m.resp_cols.data(), n, dst, n * m.fout, _s), "srpc_gpu_pack");
+            mark("pack");
             if (!whole)
                 check_srpc(srpc_frames_scatter(dst, d_idx + static_cast<uint64_t>(k) * nf, n,
                                                static_cast<uint32_t>(m.fout), d_out_off, static_cast<uint8_t*>(_d_out),
@@ -356,13 +448,18 @@ private:
                            "srpc_frames_scatter");
         }
         if (total) check(hipMemcpyAsync(_h_out, _d_out, total, hipMemcpyDeviceToHost, _s));
+        mark("d2h_out");
         if (unknown) check(hipMemcpyAsync(_h_cls, _d_cls, nf, hipMemcpyDeviceToHost, _s));
         check(hipMemcpyAsync(_h_status, _d_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
+        mark("d2h");
         check(hipStreamSynchronize(_s));
+        mark("sync2");
         // classification already matched every prefix and length: an unpack
         // status here means the buckets and the plans disagree
         if (_h_status->flags) throw plan_error("batch_server: classified frame failed to unpack", SRPC_E_INVALID);
-        st.gpu_seconds += secs(t0);
+        const double dt = secs(t0);
+        if (st.gpu_batches == 0 && st.fallback_requests == 0) st.first_batch_seconds = dt;
+        st.gpu_seconds += dt;
         st.h2d_bytes += used + 4 * nf;
         st.d2h_bytes += total + (unknown ? nf : 0);
         if (total) {
@@ -487,6 +584,7 @@ private:
     std::vector<piece> _pieces;
     std::vector<uint8_t> _flat;
     uint64_t _cap = 0, _scratch_bytes = 0;
+    bool _trace = std::getenv("SRPC_SERVER_TRACE") != nullptr;  // per-recv / per-batch timeline on stderr
     uint8_t* _h_in = nullptr;
     uint32_t* _h_offs = nullptr;
     uint8_t* _h_out = nullptr;

@@ -165,6 +165,7 @@ int main(int argc, char** argv) {
     std::string poison_method = "Calculator_servicer::squarX";  // same frame length as square's
     int64_t oversize = -1;
     double mix = 0, foreign = 0;
+    int watchdog_s = 60;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -181,6 +182,7 @@ int main(int argc, char** argv) {
         else if (a == "--mix") mix = std::stod(next());
         else if (a == "--foreign") foreign = std::stod(next());
         else if (a == "--gpu-methods") gpu_methods = next();
+        else if (a == "--watchdog") watchdog_s = std::stoi(next());
     }
     srpc::message_registry["Number"] = []() -> std::unique_ptr<Number> { return std::make_unique<Number>(); };
     srpc::message_registry["TwoNumbers"] = []() -> std::unique_ptr<TwoNumbers> {
@@ -257,8 +259,14 @@ int main(int argc, char** argv) {
         int big = 8 << 20;
         setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof(big));
         setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
-        if (gsrv) stats = gsrv->serve_connection(fd);
-        else cpu_served = cpu_server.serve_connection(fd);
+        try {
+            if (gsrv) stats = gsrv->serve_connection(fd);
+            else cpu_served = cpu_server.serve_connection(fd);
+        } catch (std::exception const& e) {
+            std::fprintf(stderr, "server: %s\n", e.what());
+            std::fflush(stderr);
+            std::_Exit(6);
+        }
         close(fd);
     });
 
@@ -270,9 +278,39 @@ int main(int argc, char** argv) {
     setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
     std::vector<uint8_t> resp(resp_total);
     auto t0 = std::chrono::steady_clock::now();
-    std::thread sender([&] { srpc::transport::send_all(fd, frames.data(), frames.size()); });
-    const bool got_all = srpc::transport::recv_all(fd, resp.data(), resp.size());
+    std::atomic<uint64_t> sent{0}, got{0};
+    std::atomic<bool> done{false};
+    std::thread sender([&] {
+        for (uint64_t o = 0; o < frames.size();) {  // send_all, with progress for the watchdog
+            const uint64_t k = std::min<uint64_t>(frames.size() - o, 1u << 20);
+            if (!srpc::transport::send_all(fd, frames.data() + o, k)) break;
+            o += k;
+            sent = o;
+        }
+    });
+    // a run that stalls says where it stalled instead of hanging until killed
+    std::thread watchdog([&] {
+        for (int i = 0; i < watchdog_s * 10 && !done; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        if (done) return;
+        std::fprintf(stderr, "WATCHDOG: %d s: client sent %llu of %zu request bytes, received %llu of %llu response bytes\n",
+                     watchdog_s, (unsigned long long)sent.load(), frames.size(), (unsigned long long)got.load(),
+                     (unsigned long long)resp_total);
+        std::fflush(stderr);
+        std::_Exit(5);
+    });
+    bool got_all = true;
+    for (uint64_t o = 0; o < resp.size();) {
+        const uint64_t k = std::min<uint64_t>(resp.size() - o, 1u << 20);
+        if (!srpc::transport::recv_all(fd, resp.data() + o, k)) {
+            got_all = false;
+            break;
+        }
+        o += k;
+        got = o;
+    }
     auto t1 = std::chrono::steady_clock::now();
+    done = true;
+    watchdog.join();
     sender.join();
     shutdown(fd, SHUT_WR);
     close(fd);
@@ -313,7 +351,7 @@ int main(int argc, char** argv) {
         "\"poison\": %llu, \"oversize\": %llu, \"mix\": %.4f, \"foreign\": %.4f, \"gpu_methods\": \"%s\"}, "
         "\"gpu\": {\"batches\": %llu, \"mixed_batches\": %llu, \"batch_frames\": %llu, \"buffer_bytes\": %llu, "
         "\"gpu_requests\": %llu, \"fallback_requests\": %llu, \"oversize_requests\": %llu, "
-        "\"gpu_seconds\": %.6f, \"fallback_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, "
+        "\"gpu_seconds\": %.6f, \"classify_seconds\": %.6f, \"first_batch_seconds\": %.6f, \"fallback_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, "
         "\"recv_seconds\": %.6f, \"send_seconds\": %.6f, \"gpu_requests_per_s\": %.1f}, \"cpu_served\": %zu}\n",
         mode.c_str(), (unsigned long long)n, (got_all && bad == 0) ? "true" : "false", (unsigned long long)bad, secs,
         n / secs, frames.size(), frames.size() / secs / 1e6, (unsigned long long)counts[SQUARE],
@@ -322,7 +360,7 @@ int main(int argc, char** argv) {
         foreign, gpu_methods.c_str(), (unsigned long long)stats.gpu_batches, (unsigned long long)stats.mixed_batches,
         (unsigned long long)batch, (unsigned long long)buffer_bytes, (unsigned long long)stats.gpu_requests,
         (unsigned long long)stats.fallback_requests, (unsigned long long)stats.oversize_requests, stats.gpu_seconds,
-        stats.fallback_seconds, (unsigned long long)stats.h2d_bytes, (unsigned long long)stats.d2h_bytes,
+        stats.classify_seconds, stats.first_batch_seconds, stats.fallback_seconds, (unsigned long long)stats.h2d_bytes, (unsigned long long)stats.d2h_bytes,
         stats.recv_seconds, stats.send_seconds,
         stats.gpu_seconds > 0 ? stats.gpu_requests / stats.gpu_seconds : 0.0, cpu_served);
     return (got_all && bad == 0) ? 0 : 1;
