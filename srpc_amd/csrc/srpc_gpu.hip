@@ -365,8 +365,16 @@ struct FieldLds {
     uint32_t size, lg, off, pad;
 };
 
+#ifndef SRPC_FLAT_WAVES
+#define SRPC_FLAT_WAVES 0  // A/B: amdgpu_waves_per_eu floor for the flat pack (0 = compiler's choice)
+#endif
+#if SRPC_FLAT_WAVES
+#define SRPC_FLAT_ATTR __attribute__((amdgpu_waves_per_eu(SRPC_FLAT_WAVES)))
+#else
+#define SRPC_FLAT_ATTR
+#endif
 template <int K>
-__global__ __launch_bounds__(kBlock) void k_pack_tile_flat(TileArgs a, uint8_t* __restrict__ wire, uint64_t n,
+__global__ __launch_bounds__(kBlock) SRPC_FLAT_ATTR void k_pack_tile_flat(TileArgs a, uint8_t* __restrict__ wire, uint64_t n,
                                                            uint64_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t T = a.R * a.stride;

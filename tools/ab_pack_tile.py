@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sizes", default="8192,12288,16384,24576,32768")
+    ap.add_argument("--cases", default="request53,response19,quad16_tile")
     args = ap.parse_args()
     import torch
 
@@ -36,7 +37,10 @@ def main():
         "request53": (NUMBER, srpc_amd.request_prefix(SQUARE_METHOD, "Number")),
         "response19": (NUMBER, srpc_amd.response_prefix(0, "Number")),
         "quad16_tile": (QUAD, b""),
+        "all_kinds17": (srpc_amd.Schema.of("all_kinds", ("a", "bool"), ("b", "int8"), ("c", "char"),
+                                           ("d", "int16"), ("e", "int32"), ("f", "int64")), b""),
     }
+    cases = {k: v for k, v in cases.items() if k in args.cases.split(",")}
     sizes = [int(x) for x in args.sizes.split(",")]
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
@@ -45,7 +49,10 @@ def main():
     for name, (sch, pre) in cases.items():
         p = GpuPacker(sch, pre)
         p.force_path(srpc_amd.SRPC_PATH_TILE)
-        cols = [torch.from_numpy(c).to(dev) for c in oracle.splitmix_columns_i32(len(sch.kinds), n)]
+        import numpy as np
+        rng = np.random.default_rng(1)
+        cols = [torch.from_numpy(rng.integers(0, 2 if k == oracle.BOOL else 256, n * oracle.KIND_SIZE[k],
+                                              dtype=np.uint8)).to(dev) for k in sch.kinds]
         wire = torch.empty(n * p.record_bytes + 16, dtype=torch.uint8, device=dev)
         back = [torch.empty_like(c) for c in cols]
         res = {}
