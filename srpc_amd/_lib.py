@@ -29,6 +29,8 @@ SRPC_STATUS_STALLED = 4
 SRPC_COMM_ID_BYTES = 128
 SRPC_MAX_FIELDS = 32
 SRPC_MAX_PREFIX = 1024
+SRPC_FRAMES_MAX_PLANS = 16
+SRPC_FRAME_UNKNOWN = 0xFF
 
 SRPC_PATH_DWORD = 1
 SRPC_PATH_TILE = 2

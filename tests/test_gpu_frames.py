@@ -135,3 +135,37 @@ def test_rejects_bad_arguments(classifier):
     rc = L.srpc_frames_classify(plans, rb, 1, buf.data_ptr(), 8, buf.data_ptr(), 1, buf.data_ptr(), buf.data_ptr(),
                                 buf.data_ptr(), buf.data_ptr(), buf.data_ptr(), 4096, None)
     assert rc == srpc_amd._lib.SRPC_E_INVALID
+
+
+def test_sixteen_methods_one_body():
+    """SRPC_FRAMES_MAX_PLANS plans of the same body size (frames differ only in
+    the method name): every bucket gets exactly its frames."""
+    K = srpc_amd._lib.SRPC_FRAMES_MAX_PLANS
+    methods = [(srpc_amd.NUMBER, f"Svc_servicer::m{k:02d}", 23) for k in range(K)]
+    plans = [GpuPacker(s, framed_request_prefix(s, m)) for s, m, _ in methods]
+    fc = FrameClassifier([(p, rb) for p, (_, _, rb) in zip(plans, methods)])
+    n = 9001
+    rng = np.random.default_rng(16)
+    want = rng.integers(0, K + 1, n)  # K = a foreign method
+    pres = [framed_request_prefix(s, m) for s, m, _ in methods]
+    foreign = framed_request_prefix(srpc_amd.NUMBER, "Svc_servicer::zzz")
+    assert all(len(q) == len(foreign) for q in pres)
+    parts = [(pres[k] if k < K else foreign) + rng.bytes(4) for k in want]
+    buf = b"".join(parts)
+    offs = (np.arange(n, dtype=np.uint32) * len(parts[0])).astype(np.uint32)
+    d_buf, d_offs = dev(np.frombuffer(buf, np.uint8)), dev(offs)
+    d_cls, d_idx = empty(n + 16), empty(4 * K * n + 16)
+    d_counts, d_out_off = empty(8 * (K + 2)), empty(8 * (n + 1))
+    sb = fc.scratch_bytes(n)
+    scratch = torch.empty(sb, dtype=torch.uint8, device="cuda:0")
+    fc.classify(d_buf, len(buf), d_offs, n, d_cls, d_idx, d_counts, d_out_off, scratch, sb)
+    counts = host(d_counts, 8 * (K + 2), np.uint64)
+    cls = host(d_cls, n)
+    exp_cls = np.where(want == K, UNKNOWN, want).astype(np.uint8)
+    assert np.array_equal(cls, exp_cls)
+    idx = host(d_idx, 4 * K * n, np.uint32).reshape(K, n)
+    for k in range(K):
+        nk = int(counts[k])
+        assert nk == int((want == k).sum())
+        assert np.array_equal(np.sort(idx[k, :nk]), np.flatnonzero(want == k).astype(np.uint32))
+    assert int(counts[K + 1]) == int((want == K).sum()) and int(counts[K]) == 23 * int((want < K).sum())

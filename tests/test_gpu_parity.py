@@ -167,6 +167,30 @@ def test_random_schemas_vs_oracle(n, schema):
             assert a.tobytes() == b.tobytes()
 
 
+@pytest.mark.parametrize("n", [1, 3, 5, 4097, 65539])
+@pytest.mark.parametrize("kinds,prefix", [
+    ([oracle.INT16, oracle.INT64], b"abc"),  # 13 B, G = 4, prefix bytes inside a group's dwords
+    ([oracle.INT64, oracle.INT64, oracle.INT64, oracle.INT32, oracle.INT8], b""),  # 29 B, 32-byte column loads
+    ([oracle.INT8, oracle.INT16, oracle.INT8, oracle.INT32, oracle.INT8, oracle.INT64], b"\x01\x02"),  # 19 B
+    ([oracle.INT16, oracle.INT32], b"q" * 24),  # 30 B, G = 2, mostly prefix
+])
+def test_odd_stride_register_groups_vs_oracle(n, kinds, prefix):
+    """Small records whose stride is not a multiple of 4 (the TILE pack's
+    register-assembled groups): sizes that leave a partial last group, a
+    partial last tile and a ragged wire tail, with and without an envelope."""
+    rng = np.random.default_rng(n * 7 + len(kinds) + len(prefix))
+    cols = [rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(oracle.KIND_DTYPE[k])
+            for k in kinds]
+    p = GpuPacker(Schema("X", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    assert p.path == SRPC_PATH_TILE
+    want = oracle.pack(kinds, cols, n, prefix)
+    assert gpu_pack(p, cols, n) == want
+    rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+    assert rc == 0
+    for a, b in zip(cols, back):
+        assert a.tobytes() == b.tobytes()
+
+
 @pytest.mark.parametrize("n", [1, 1000, 20_001])
 @pytest.mark.parametrize("strings", [False, True])
 def test_schema_at_the_limits_vs_oracle(n, strings):

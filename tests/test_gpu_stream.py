@@ -214,3 +214,18 @@ def test_trailing_bytes_after_n_records():
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n)[:m + 1])
     for f, k in enumerate(kinds):
         assert back[f].tobytes() == ocols[f].tobytes(), f
+
+
+@pytest.mark.parametrize("prefix", [b"\x07", b"abc", b"1234567", b"12345678"])
+def test_short_custom_prefixes(prefix):
+    """Prefixes shorter than the 8-byte filter word (and exactly 8): the scan's
+    prefix filter masks the bytes it compares; plausibility then needs two
+    records (a bare or short prefix) or one (8 bytes or more)."""
+    kinds = KINDS["mixed"]
+    n = 7001
+    rng = np.random.default_rng(len(prefix))
+    cols, offs = _random_string_batch(kinds, n, rng, 40)
+    p = GpuPacker(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    wire = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
