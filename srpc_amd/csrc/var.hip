@@ -1047,6 +1047,292 @@ __device__ __forceinline__ void lds_copy_run(uint8_t* lds, uint32_t d, uint32_t 
     while (len--) lds[d++] = lds[s++];
 }
 
+// A workgroup is resident for the whole batch and takes tiles t, t + G, ...
+// (G = the grid, sized by the host to what the chip holds at once), software
+// pipelined so that its loads and stores overlap instead of following each
+// other: the global values of tile t + G's staging table are loaded while tile
+// t's stage is awaited, its granules are requested by LDS-DMA right after tile
+// t's image stores are issued, and one wait covers both.  The barriers inside
+// the loop wait on LDS only (lds_barrier): a __syncthreads() would also wait
+// for every store in flight (vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void vm_wait_all() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Per-tile values of the staging table (double-buffered: tile t + G's are
+// written while tile t's are read).
+struct RtTile {
+    uint64_t base;                // wire offset of the tile's first record
+    uint32_t fits;                // every region incl. the chars is staged
+    uint32_t fsw[kMaxFields];     // string ordinal -> LDS offset of its window entry 0
+    uint32_t fch[kMaxFields];     // string ordinal -> LDS offset of char soff[f][r0]
+    uint32_t ffx[kMaxFields];     // fixed ordinal -> LDS offset of its value of record r0
+};
+
+// Lane g of wave 0 describes region g of every tile: string ordinal g's
+// offsets window (g < ns), fixed ordinal g - ns's column slice, string
+// ordinal g - ns - nfx's chars.  Resolved once per workgroup: indexing the
+// kernel arguments by lane is a chain of dependent vector loads.
+struct RtLane {
+    uint32_t kind = 0;  // 1 offsets window, 2 chars, 3 fixed column slice
+    uint32_t ord = 0;
+    uint32_t sz = 0;
+    const uint64_t* so = nullptr;
+    const uint8_t* col = nullptr;
+};
+__device__ __forceinline__ RtLane rt_lane(const VarArgs& a, uint32_t g) {
+    RtLane r;
+    const uint32_t ns = a.nstrings, nfx = a.nfields - a.nstrings;
+    if (g < ns) {
+        r.kind = 1;
+        r.ord = g;
+        r.so = a.soff[a.sfield[g]];
+    } else if (g < ns + nfx) {
+        r.kind = 3;
+        r.ord = g - ns;
+        const uint32_t f = a.ffield[r.ord];
+        r.col = a.col[f];
+        r.sz = a.size[f];
+    } else if (g < 2 * ns + nfx) {
+        r.kind = 2;
+        r.ord = g - ns - nfx;
+        const uint32_t f = a.sfield[r.ord];
+        r.so = a.soff[f];
+        r.col = a.col[f];
+    }
+    return r;
+}
+
+// The global values a lane needs for tile t's table: its string's soff[r0]
+// and soff[0] (offsets window: the chars before the tile), or soff[r0] and
+// soff[r0 + nr] (chars range).  Issued a tile ahead; used after a wait.
+struct RtPend {
+    uint64_t x0, x1;
+};
+__device__ __forceinline__ RtPend rt_issue(const RtLane& R, uint64_t n, uint64_t t) {
+    RtPend v{0, 0};
+    const uint64_t r0 = t * kBlock;
+    const uint64_t nr = min<uint64_t>(kBlock, n - r0);
+    if (R.kind == 1 || R.kind == 2) {
+        v.x0 = R.so[r0];
+        v.x1 = R.so[R.kind == 1 ? 0 : r0 + nr];
+    }
+    return v;
+}
+
+// Wave 0, one lane per region: region g's granules land in the stage in
+// granule order, granule x at stage_at + 16 x.
+__device__ __forceinline__ void rt_table(const RtLane& R, uint64_t fixed_bytes, const RtArgs& L, uint32_t stage_at,
+                                         uint64_t n, uint64_t t, uint32_t g, RtPend v, RtTile& T, RtRegion* rt,
+                                         uint32_t* s_ngran) {
+    const uint64_t r0 = t * kBlock;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
+    uint64_t lo = 0, hi = 0;
+    uint64_t before = 0;  // chars of this string field in the records before the tile
+    if (R.kind == 1) {
+        lo = reinterpret_cast<uint64_t>(R.so + r0);
+        hi = reinterpret_cast<uint64_t>(R.so + r0 + nr + 1);
+        before = v.x0 - v.x1;
+    } else if (R.kind == 3) {
+        lo = reinterpret_cast<uint64_t>(R.col + r0 * R.sz);
+        hi = lo + static_cast<uint64_t>(nr) * R.sz;
+    } else if (R.kind == 2) {
+        lo = reinterpret_cast<uint64_t>(R.col + v.x0);
+        hi = reinterpret_cast<uint64_t>(R.col + v.x1);
+    }
+    // record r starts at r * fixed_bytes + sum over string fields of
+    // (soff[r] - soff[0]): the wire offsets need no scan
+    const uint64_t chars_before = __shfl(wave_inclusive_scan(before), 63, 64);
+    if (g == 0) T.base = r0 * fixed_bytes + chars_before;
+    const uint64_t A = lo & ~15ull;
+    uint64_t ng = hi > lo ? (hi - A + 15) >> 4 : 0;
+    uint64_t inc = wave_inclusive_scan(ng);
+    // the chars regions come last: when everything does not fit the stage,
+    // the chars are not staged and the tile takes the global walk
+    const bool fits = 16 * __shfl(inc, 63, 64) <= L.stage_cap;
+    if (!fits) {
+        if (R.kind == 2) ng = 0;
+        inc = wave_inclusive_scan(ng);
+    }
+    if (R.kind) {
+        const uint32_t g0 = static_cast<uint32_t>(inc - ng);
+        rt[g] = {A, g0, 0};
+        const uint32_t at = stage_at + 16 * g0 + static_cast<uint32_t>(lo - A);
+        if (R.kind == 1) T.fsw[R.ord] = at;
+        else if (R.kind == 2) T.fch[R.ord] = at;
+        else T.ffx[R.ord] = at;
+    }
+    if (g == 63) {
+        *s_ngran = static_cast<uint32_t>(inc);
+        T.fits = fits;
+    }
+}
+
+// Granules -> stage by LDS-DMA (global_load_lds_dwordx4: a wave instruction
+// fills 1 KiB of LDS lane-linearly, no VGPRs hold the data, nothing waits
+// here); a lane's granules increase, so its region index only moves forward.
+__device__ __forceinline__ void rt_dma(uint32_t stage_at, uint32_t nreg, uint32_t ngran, const RtRegion* rt,
+                                       uint8_t* lds) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t r = 0;
+    for (uint32_t w0 = threadIdx.x & ~63u; w0 < ngran; w0 += kBlock) {
+        const uint32_t gi = w0 + lane;
+        if (gi < ngran) {
+            while (r + 1 < nreg && rt[r + 1].g0 <= gi) ++r;
+            const uint64_t src = rt[r].src + 16ull * (gi - rt[r].g0);
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src),
+                                             (lds_u8*)(lds + stage_at + 16 * wb), 16, 0, 0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_var_rt_loop(VarArgs a, RtArgs L, uint64_t n, uint8_t* __restrict__ wire,
+                                                        uint64_t wire_cap, uint64_t* __restrict__ rec_offs,
+                                                        srpc_unpack_status* st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ RtRegion rt[kRtRegions];
+    __shared__ RtTile tl[2];
+    __shared__ uint64_t lofs[kBlock + 1];     // local record starts (image positions minus h), [nr] = total
+    __shared__ uint64_t climit[kMaxFields];   // string field: soff[f][n] (end of its chars)
+    __shared__ uint32_t s_ngran;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ns = a.nstrings, nreg = 2 * ns + (a.nfields - a.nstrings);
+    const uint64_t ntiles = (n + kBlock - 1) / kBlock;
+    uint64_t t = blockIdx.x;
+    // prefix + 32 zero bytes (emit_record reads 16 bytes at any prefix offset)
+    for (uint32_t i = threadIdx.x; i < a.prefix_len + 32; i += kBlock)
+        lds[L.pre_at + i] = i < a.prefix_len ? a.prefix[i] : 0;
+    for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
+    RtLane R;
+    if (threadIdx.x < 64) {
+        R = rt_lane(a, lane);
+        rt_table(R, a.fixed_bytes, L, L.stage_at, n, t, lane, rt_issue(R, n, t), tl[0], rt, &s_ngran);
+    }
+    __syncthreads();
+    rt_dma(L.stage_at, nreg, s_ngran, rt, lds);
+    for (uint32_t b = 0; t < ntiles; t += gridDim.x, b ^= 1) {
+        const uint64_t tn = t + gridDim.x;
+        const bool more = tn < ntiles;
+        RtPend pend{0, 0};
+        if (more && threadIdx.x < 64) pend = rt_issue(R, n, tn);
+        vm_wait_all();  // this tile's granules (and the last tile's stores)
+        lds_barrier();
+        if (more && threadIdx.x < 64)
+            rt_table(R, a.fixed_bytes, L, L.stage_at, n, tn, lane, pend, tl[b ^ 1], rt, &s_ngran);
+        const RtTile& T = tl[b];
+        const uint64_t r0 = t * kBlock;
+        const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
+        // record starts from the staged offsets windows
+        const uint32_t i = threadIdx.x;
+        if (i < nr) {
+            uint64_t e = static_cast<uint64_t>(i + 1) * a.fixed_bytes;
+            for (uint32_t si = 0; si < ns; ++si) {
+                const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + T.fsw[si]);
+                e += w[i + 1] - w[0];
+            }
+            lofs[i + 1] = e;
+        }
+        if (i == 0) lofs[0] = 0;
+        lds_barrier();
+        const uint64_t base = T.base, total = lofs[nr];
+        if (i < nr) {
+            const uint64_t start = base + lofs[i], end = base + lofs[i + 1];
+            rec_offs[r0 + i] = start;
+            if (st && start <= wire_cap && wire_cap < end) report_bad(st, SRPC_STATUS_BOUNDS, r0 + i);
+        }
+        if (i == 0 && r0 + nr == n) rec_offs[n] = base + total;
+        const uint32_t h = static_cast<uint32_t>(base & 15);
+        const uint64_t gbase = base & ~15ull;
+        const uint64_t wend = min(base + total, wire_cap);  // wire bytes of this tile end here
+        uint8_t* img = lds + L.img_at;
+        if (T.fits && h + total <= L.img_cap) {
+            // records -> LDS image
+            if (i < nr) {
+                uint32_t d = L.img_at + h + static_cast<uint32_t>(lofs[i]);
+                if (a.prefix_len) {
+                    lds_copy_run(lds, d, L.pre_at, a.prefix_len);
+                    d += a.prefix_len;
+                }
+                uint32_t si = 0, fi = 0;
+                for (uint32_t f = 0; f < a.nfields; ++f) {
+                    const uint32_t sz = a.size[f];
+                    if (sz) {
+                        const uint8_t* v = lds + T.ffx[fi++] + i * sz;
+                        const uint64_t x = sz == 1   ? *v
+                                           : sz == 2 ? load_unaligned<uint16_t>(v)
+                                           : sz == 4 ? load_unaligned<uint32_t>(v)
+                                                     : load_unaligned<uint64_t>(v);
+                        lds_put_small(lds, d, x, sz);
+                        d += sz;
+                        continue;
+                    }
+                    const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + T.fsw[si]);
+                    const uint64_t c0 = w[0], cb = w[i], len = w[i + 1] - cb;
+                    lds_put_small(lds, d, len, 8);
+                    d += 8;
+                    lds_copy_run(lds, d, T.fch[si] + static_cast<uint32_t>(cb - c0), static_cast<uint32_t>(len));
+                    d += static_cast<uint32_t>(len);
+                    ++si;
+                }
+            }
+            lds_barrier();  // image complete; the stage is free for the next tile
+            // image -> wire
+            const uint32_t span = h + static_cast<uint32_t>(total);
+            const uint32_t nch = (span + 15) >> 4;
+            for (uint32_t c = threadIdx.x; c < nch; c += kBlock) {
+                const uint64_t g = gbase + 16ull * c;
+                const uint32_t lo = max(h, 16 * c), hi = min(span, 16 * c + 16);
+                if (lo == 16 * c && hi == 16 * c + 16 && g + 16 <= wire_cap) {
+                    const u64x2 v = *reinterpret_cast<const u64x2*>(img + 16 * c);
+                    __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(wire + g));
+                } else {
+                    for (uint32_t x = lo; x < hi && gbase + x < wend; ++x) wire[gbase + x] = img[x];
+                }
+            }
+        } else {
+            // span or chars too large for LDS: chunk walk over [base, base + total)
+            // with global sources; the image region holds the lanes' 32-byte slots
+            uint32_t f0 = 0;
+            while (a.size[f0]) ++f0;
+            Slot c{img + 32 * threadIdx.x};
+            for (uint64_t p0 = gbase + 16ull * threadIdx.x; p0 < wend; p0 += 16ull * kBlock) {
+                const uint64_t lo = max(p0, base), hi = min(p0 + 16, wend);
+                if (lo >= hi) continue;
+                // last record whose start <= lo (records may be empty)
+                uint32_t k0 = 0, k1 = nr;  // lofs[k0] + base <= lo < lofs[k1] + base
+                while (k1 - k0 > 1) {
+                    const uint32_t mid = (k0 + k1) >> 1;
+                    if (base + lofs[mid] <= lo) k0 = mid;
+                    else k1 = mid;
+                }
+                uint64_t p = lo;
+                uint32_t b2 = static_cast<uint32_t>(lo - p0);
+                for (uint32_t k = k0; p < hi && k < nr; ++k) {
+                    const uint64_t rs = base + lofs[k], re = base + lofs[k + 1];
+                    if (re <= p) continue;
+                    const uint32_t cnt = static_cast<uint32_t>(min(hi, re) - p);
+                    emit_record(a, lds + L.pre_at, climit, f0, nullptr, n, r0 + k, p - rs, cnt, static_cast<int>(b2), c);
+                    b2 += cnt;
+                    p += cnt;
+                }
+                if (lo == p0 && hi == p0 + 16) {
+                    store_slot(wire + p0, c, 16);
+                } else {
+                    for (uint64_t x = lo; x < hi; ++x) wire[x] = c.s[x - p0];
+                }
+            }
+        }
+        if (more) rt_dma(L.stage_at, nreg, s_ngran, rt, lds);
+    }
+}
+
+// One tile per workgroup (records under kRtPersistMin bytes on average: the
+// loop kernel's per-tile barriers and wider register state cost more than
+// its overlap saves on 4-8 KiB tiles, profiles/r02_var_rt_persist_ab.log).
 __global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uint64_t n, uint8_t* __restrict__ wire,
                                                         uint64_t wire_cap, uint64_t* __restrict__ rec_offs,
                                                         srpc_unpack_status* st) {
@@ -1822,6 +2108,27 @@ ScratchLayout scratch_layout(const srpc_plan* p, uint64_t n, uint64_t wire_bytes
 
 uint32_t round16(uint32_t b) { return (b + 15) & ~15u; }
 
+// Workgroups of `kernel` (kBlock threads, `lds` dynamic LDS bytes) the device
+// holds at once, times SRPC_RT_GRID_MULT (A/B builds; default 1).
+#ifndef SRPC_RT_GRID_MULT
+#define SRPC_RT_GRID_MULT 1
+#endif
+#ifndef SRPC_RT_PERSIST_MIN
+#define SRPC_RT_PERSIST_MIN 40
+#endif
+constexpr uint64_t kRtPersistMin = SRPC_RT_PERSIST_MIN;
+template <typename K>
+uint64_t resident_grid(K kernel, uint32_t lds, int device) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || per_cu < 1 ||
+        cus < 1) {
+        per_cu = 2;
+        cus = 256;
+    }
+    return static_cast<uint64_t>(per_cu) * cus * SRPC_RT_GRID_MULT;
+}
+
 // LDS carve of k_pack_var_rt (see RtArgs).  The image holds a tile's wire
 // span: 256 records of `avg` bytes (the caller's wire_cap / n, exact when the
 // caller sizes the wire buffer to the batch) with 1/16 slack, unless the plan
@@ -1951,9 +2258,22 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
         if (ntiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
         if (!wire) return SRPC_E_INVALID;
         uint32_t lds = 0;
+        const bool loop = wire_cap / n >= kRtPersistMin;
         const RtArgs R = rt_layout(p, wire_cap / n, &lds);
-        launch(k_pack_var_rt, dim3(static_cast<uint32_t>(ntiles)), dim3(kBlock), lds, s, a, R, n, wire, wire_cap,
-               rec_offs, st);
+        // records of >= SRPC_RT_PERSIST_MIN bytes on average: resident workgroups
+        // only, each looping over its tiles with the next tile's loads in flight
+        // (two strings + request envelope 228 -> 193 us, 0-64 B 134 -> 127 us);
+        // shorter records: a workgroup per tile, as the loop's per-tile barriers
+        // cost more than the overlap saves on 4-8 KiB tiles (0-16 B strings
+        // 112 -> 134 us persistent, profiles/r02_var_rt_persist_ab.log)
+        if (loop) {
+            const uint64_t grid = std::min<uint64_t>(ntiles, resident_grid(k_pack_var_rt_loop, lds, p->device));
+            launch(k_pack_var_rt_loop, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), lds, s, a, R, n, wire,
+                   wire_cap, rec_offs, st);
+        } else {
+            launch(k_pack_var_rt, dim3(static_cast<uint32_t>(ntiles)), dim3(kBlock), lds, s, a, R, n, wire,
+                   wire_cap, rec_offs, st);
+        }
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     auto* tiles = reinterpret_cast<uint64_t*>(base + L.tiles_off);
