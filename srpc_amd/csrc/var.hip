@@ -1644,19 +1644,19 @@ __device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2,
 
 struct RtuArgs {
     uint32_t pre_at;     // prefix + 16 bytes
-    uint32_t stage_at;   // index window granules (kRtWin bytes), then the wire span's (stage_cap bytes)
-    uint32_t pos_at;     // per string ordinal: 256 u64 chars positions (wire offsets)
+    uint32_t stage_at;   // the wire span's granules (stage_cap bytes)
     uint32_t len_at;     // per string ordinal: 256 u64 lengths, then offsets inside the tile's chars
     uint32_t img_at;     // chars image, img_cap bytes
     uint32_t stage_cap, img_cap;
 };
 
 // General decode of record r (walk_record's multi-string semantics); string
-// ordinal si's chars position and length go to pos/len[si * 256 + lane].
+// ordinal si's length goes to len_l[si * 256 + lane] (its chars position is
+// found again by string_pos when the chars are copied).
 template <typename Pre>
 __device__ __forceinline__ uint32_t parse_record(const VarArgs& a, const uint8_t* src, const Pre* pre, uint64_t r,
-                                                 uint64_t start, uint64_t end, uint64_t wire_len, uint64_t* pos_l,
-                                                 uint64_t* len_l, uint32_t i) {
+                                                 uint64_t start, uint64_t end, uint64_t wire_len, uint64_t* len_l,
+                                                 uint32_t i) {
     uint32_t flag = 0;
     if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
     if (!flag) {
@@ -1695,7 +1695,6 @@ __device__ __forceinline__ uint32_t parse_record(const VarArgs& a, const uint8_t
         } else {
             flag = SRPC_STATUS_BOUNDS;
         }
-        pos_l[si * kBlock + i] = pos;
         len_l[si * kBlock + i] = len;
         ++si;
         pos += len;
@@ -1706,11 +1705,32 @@ __device__ __forceinline__ uint32_t parse_record(const VarArgs& a, const uint8_t
     return flag;
 }
 
+// Wire offset of string ordinal si's chars in a record that decoded without a
+// BOUNDS error (every length fits the record), walking its fields again;
+// rd(p) reads the u64 at wire offset p (the LDS stage or global memory).
+template <class Rd>
+__device__ __forceinline__ uint64_t string_pos(const VarArgs& a, uint64_t start, uint32_t si, Rd rd) {
+    uint64_t pos = start + a.prefix_len;
+    uint32_t k = 0;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            pos += sz;
+            continue;
+        }
+        const uint64_t len = rd(pos);
+        pos += 8;
+        if (k++ == si) break;
+        pos += len;
+    }
+    return pos;
+}
+
 // parse_record for a record staged in LDS at byte offset `so` (wire offset
 // `start`), the prefix at LDS offset `po` (16-aligned): every read is aligned.
 __device__ __forceinline__ uint32_t parse_record_lds(const VarArgs& a, const uint8_t* lds, uint32_t so, uint32_t po,
                                                      uint64_t r, uint64_t start, uint64_t end, uint64_t wire_len,
-                                                     uint64_t* pos_l, uint64_t* len_l, uint32_t i) {
+                                                     uint64_t* len_l, uint32_t i) {
     uint32_t flag = 0;
     if (start > end || end > wire_len || end - start < a.fixed_bytes) flag = SRPC_STATUS_BOUNDS;
     if (!flag && a.prefix_len) {
@@ -1757,7 +1777,6 @@ __device__ __forceinline__ uint32_t parse_record_lds(const VarArgs& a, const uin
         } else {
             flag = SRPC_STATUS_BOUNDS;
         }
-        pos_l[si * kBlock + i] = pos;
         len_l[si * kBlock + i] = len;
         ++si;
         pos += len;
@@ -1783,96 +1802,87 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
                                                           srpc_unpack_status* st, uint32_t* __restrict__ bad) {
     if constexpr (!kOpt)
         if (bad && *bad == 0) return;  // the optimistic pass was exact everywhere
+    PHASE_BEGIN
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ RtRegion rt[2];
-    __shared__ uint64_t s_tile, s_lo, s_hi, s_base, s_first;
+    __shared__ uint64_t s_tile, s_lo, s_hi, s_src, s_first;
     __shared__ uint32_t s_inexact;
     __shared__ uint64_t s_tot[kMaxFields], s_pre[kMaxFields];
     __shared__ uint32_t s_ioff[kMaxFields];
-    __shared__ uint32_t s_ngran, s_staged, s_fits;
+    __shared__ uint32_t s_ngran, s_fits;
     const uint32_t lane = threadIdx.x & 63, i = threadIdx.x;
     const uint32_t ns = a.nstrings;
 #if SRPC_RTU_TICKET
     if (i == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t t = s_tile;
 #else
     // tile = blockIdx.x: every XCD dispatches its workgroups in increasing
     // order, so the smallest unfinished tile is always resident and every
     // look-back ends (one ticket atomic per tile, all on one address, cost
     // ~10 ns each at the memory side: 32K tiles -> 300 us, r02_var_rtu_ab.log);
     // the spin limit in the look-back guarantees termination regardless
-    if (i == 0) s_tile = blockIdx.x;
+    const uint64_t t = blockIdx.x;
 #endif
-    for (uint32_t k = i; k < a.prefix_len + 16; k += kBlock) lds[L.pre_at + k] = k < a.prefix_len ? a.prefix[k] : 0;
-    __syncthreads();
-    const uint64_t t = s_tile;
     const uint64_t r0 = t * kBlock;
     const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
-    // 1. staging table: region 0 the index window, region 1 the wire span
-    if (i < 64) {
-        uint64_t lo = 0, hi = 0;
-        if (lane == 0) {
-            lo = reinterpret_cast<uint64_t>(rec_offs + r0);
-            hi = reinterpret_cast<uint64_t>(rec_offs + r0 + nr + 1);
-        } else if (lane == 1) {
-            const uint64_t w0 = rec_offs[r0], w1 = rec_offs[r0 + nr];
-            s_lo = w0;
-            s_hi = w1;
-            if (kOpt) {
-                s_first = rec_offs[0];
-                s_inexact = 0;
-            }
-            if (w0 < w1 && w1 <= wire_len) {
-                lo = reinterpret_cast<uint64_t>(wire + w0);
-                hi = reinterpret_cast<uint64_t>(wire + w1);
-            }
+    // the lane's record bounds stay in registers (coalesced loads, issued
+    // with the prefix bytes and before the table's wait)
+    const uint64_t start = i < nr ? rec_offs[r0 + i] : 0, end = i < nr ? rec_offs[r0 + i + 1] : 0;
+    // the prefix's first kBlock bytes are loaded here and written to LDS after
+    // the table, so their round trip overlaps the index loads (one barrier
+    // less before the stage can be requested)
+    const uint8_t pb = i < a.prefix_len ? a.prefix[i] : 0;
+    // 1. the tile's wire span [rec_offs[r0], rec_offs[r0 + nr]) in 16-byte granules
+    if (i == 0) {
+        const uint64_t w0 = rec_offs[r0], w1 = rec_offs[r0 + nr];
+        s_lo = w0;
+        s_hi = w1;
+        if (kOpt) {
+            s_first = rec_offs[0];
+            s_inexact = 0;
         }
-        const uint64_t A = lo & ~15ull;
-        uint64_t ng = hi > lo ? (hi - A + 15) >> 4 : 0;
-        if (lane == 1 && 16 * ng > L.stage_cap) ng = 0;  // span too large: parse from global memory
-        const uint64_t inc = wave_inclusive_scan(ng);
-        if (lane < 2) {
-            rt[lane] = {A, static_cast<uint32_t>(inc - ng), 0};
-            if (lane == 1) {
-                s_staged = ng != 0;
-                s_base = A - reinterpret_cast<uint64_t>(wire);  // wire offset of the stage's first granule
-            }
+        uint64_t A = 0, ng = 0;
+        if (w0 < w1 && w1 <= wire_len) {
+            A = reinterpret_cast<uint64_t>(wire + w0) & ~15ull;
+            ng = (reinterpret_cast<uint64_t>(wire + w1) - A + 15) >> 4;
+            if (16 * ng > L.stage_cap) ng = 0;  // span too large: parse from global memory
         }
-        if (lane == 63) s_ngran = static_cast<uint32_t>(inc);
+        s_src = A;
+        s_ngran = static_cast<uint32_t>(ng);
     }
+    if (i < a.prefix_len + 16) lds[L.pre_at + i] = pb;
+    for (uint32_t k = i + kBlock; k < a.prefix_len + 16; k += kBlock)
+        lds[L.pre_at + k] = k < a.prefix_len ? a.prefix[k] : 0;
     __syncthreads();
-    {
-        const uint32_t ngran = s_ngran;
-        uint32_t r = 0;
-        for (uint32_t w0 = i & ~63u; w0 < ngran; w0 += kBlock) {
-            const uint32_t gi = w0 + lane;
-            if (gi < ngran) {
-                if (r == 0 && rt[1].g0 <= gi) r = 1;
-                const uint64_t src = rt[r].src + 16ull * (gi - rt[r].g0);
-                const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src),
-                                                 (lds_u8*)(lds + L.stage_at + 16 * wb), 16, 0, 0);
-            }
+    PHASE(0);
+    // 2. span -> stage by LDS-DMA (global_load_lds_dwordx4: a wave
+    // instruction fills 1 KiB of LDS, no VGPRs hold the data)
+    const uint32_t ngran = s_ngran;
+    const uint64_t src0 = s_src;
+    for (uint32_t w0 = i & ~63u; w0 < ngran; w0 += kBlock) {
+        const uint32_t gi = w0 + lane;
+        if (gi < ngran) {
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(src0 + 16ull * gi),
+                                             (lds_u8*)(lds + L.stage_at + 16 * wb), 16, 0, 0);
         }
     }
     __syncthreads();  // waits for the LDS-DMA (vmcnt(0)) and publishes the stage
-    const uint64_t* win = reinterpret_cast<const uint64_t*>(
-        lds + L.stage_at + static_cast<uint32_t>(reinterpret_cast<uint64_t>(rec_offs + r0) & 15));
-    const bool staged = s_staged;
+    PHASE(1);
+    const bool staged = ngran != 0;
     const uint64_t slo = s_lo, shi = s_hi;
-    // the wire span's first granule follows the window's granules
-    const uint8_t* sbase = lds + L.stage_at + 16 * rt[1].g0;
-    const uint64_t sw = s_base;  // wire offset of sbase[0]
-    uint64_t* pos_l = reinterpret_cast<uint64_t*>(lds + L.pos_at);
+    const uint32_t sb = L.stage_at;                       // LDS offset of the stage's first granule
+    const uint64_t sw = src0 - reinterpret_cast<uint64_t>(wire);  // its wire offset
     uint64_t* len_l = reinterpret_cast<uint64_t*>(lds + L.len_at);
-    // 2. parse
+    // 3. parse (the record's chars positions are walked again when copied)
+    uint32_t flag = SRPC_STATUS_BOUNDS;  // lanes past the tile: nothing to copy
+    const bool in_stage = staged && start >= slo && end <= shi && start <= end;
     if (i < nr) {
-        const uint64_t start = win[i], end = win[i + 1];
-        uint32_t flag;
-        if (staged && start >= slo && end <= shi && start <= end)
-            flag = parse_record_lds(a, lds, static_cast<uint32_t>(sbase - lds) + static_cast<uint32_t>(start - sw),
-                                    L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
+        if (in_stage)
+            flag = parse_record_lds(a, lds, sb + static_cast<uint32_t>(start - sw), L.pre_at, r0 + i, start, end,
+                                    wire_len, len_l, i);
         else
-            flag = parse_record(a, wire + start, lds + L.pre_at, r0 + i, start, end, wire_len, pos_l, len_l, i);
+            flag = parse_record(a, wire + start, lds + L.pre_at, r0 + i, start, end, wire_len, len_l, i);
         if (flag && st) report_bad(st, flag, r0 + i);
         if (kOpt && (start > end || end - start < a.fixed_bytes || len_l[i] != end - start - a.fixed_bytes))
             s_inexact = 1;
@@ -1880,7 +1890,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         for (uint32_t k = 0; k < ns; ++k) len_l[k * kBlock + i] = 0;
     }
     __syncthreads();
-    // 3. per string field: offsets inside the tile, tile totals
+    PHASE(2);
+    // per string field: offsets inside the tile, tile totals
     for (uint32_t si = 0; si < ns; ++si) {
         uint64_t tot;
         // lengths become exclusive offsets in place (len = next offset - offset)
@@ -1893,7 +1904,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     }
     if (kOpt) {  // the tile's chars base, valid when every record before it is exact
         if (i == 0) {
-            const uint64_t first = s_first, w0 = win[0];
+            const uint64_t first = s_first, w0 = start;
             const uint64_t fixed_before = r0 * a.fixed_bytes;
             const bool ok = !s_inexact && w0 >= first && w0 - first >= fixed_before &&
                             w0 - first - fixed_before <= wire_len && s_tot[0] <= wire_len - (w0 - first - fixed_before);
@@ -1918,25 +1929,40 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         s_fits = at + 16 <= L.img_cap;
     }
     __syncthreads();
+    PHASE(3);
     const bool fits = s_fits;
+    // string chars positions: from the stage for a staged record, else from global memory
+    auto rd = [&](uint64_t p) -> uint64_t {
+        return in_stage ? lds_u64(lds, sb + static_cast<uint32_t>(p - sw)) : load_unaligned<uint64_t>(wire + p);
+    };
     auto build = [&]() {
-        if (!fits || i >= nr) return;
-        for (uint32_t k = 0; k < ns; ++k) {
-            const uint64_t o = len_l[k * kBlock + i], pos = pos_l[k * kBlock + i];
+        if (!fits || flag == SRPC_STATUS_BOUNDS) return;
+        uint64_t pos = start + a.prefix_len;
+        uint32_t k = 0;
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            const uint32_t sz = a.size[f];
+            if (sz) {
+                pos += sz;
+                continue;
+            }
+            pos += 8;  // the length (the scan's offsets give it back)
+            const uint64_t o = len_l[k * kBlock + i];
             const uint64_t len = (i + 1 < kBlock ? len_l[k * kBlock + i + 1] : s_tot[k]) - o;
-            if (!len) continue;
-            const uint32_t d = L.img_at + s_ioff[k] + static_cast<uint32_t>(o);
-            if (staged && pos >= slo && pos + len <= shi) {
-                lds_copy_run(lds, d, static_cast<uint32_t>(sbase - lds) + static_cast<uint32_t>(pos - sw),
-                             static_cast<uint32_t>(len));
-            } else {
-                for (uint64_t x = 0; x < len; x += 8) {
-                    const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(8, len - x));
-                    uint64_t v = 0;
-                    for (uint32_t b = 0; b < kk; ++b) v |= static_cast<uint64_t>(wire[pos + x + b]) << (8 * b);
-                    lds_put_small(lds, d + static_cast<uint32_t>(x), v, kk);
+            if (len) {
+                const uint32_t d = L.img_at + s_ioff[k] + static_cast<uint32_t>(o);
+                if (in_stage) {
+                    lds_copy_run(lds, d, sb + static_cast<uint32_t>(pos - sw), static_cast<uint32_t>(len));
+                } else {
+                    for (uint64_t x = 0; x < len; x += 8) {
+                        const uint32_t kk = static_cast<uint32_t>(min<uint64_t>(8, len - x));
+                        uint64_t v = 0;
+                        for (uint32_t b = 0; b < kk; ++b) v |= static_cast<uint64_t>(wire[pos + x + b]) << (8 * b);
+                        lds_put_small(lds, d + static_cast<uint32_t>(x), v, kk);
+                    }
                 }
             }
+            pos += len;
+            ++k;
         }
     };
     // string field si's look-back runs on wave si mod 4: the fields' round
@@ -1955,6 +1981,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     }
     build();
     __syncthreads();
+    PHASE(4);
     // 4. str_offs and chars, per string field; chunk c of the output covers
     // image bytes [16c - h, 16c + 16 - h), h = the base's offset in its 16-byte
     // block, the same for every chunk: a uniform byte shift of two aligned
@@ -2008,16 +2035,21 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
                     for (uint32_t x = lo; x < hi; ++x) chars[gbase + x] = im[x - h];
                 }
             }
-        } else if (!SRPC_RTU_NOCHARS && i < nr) {  // the tile's chars exceed the image: copied lane by lane
-            const uint64_t pos = pos_l[si * kBlock + i];
+        } else if (!SRPC_RTU_NOCHARS && i < nr && flag != SRPC_STATUS_BOUNDS) {
+            // the tile's chars exceed the image: copied lane by lane
             const uint64_t len = (i + 1 < kBlock ? len_l[si * kBlock + i + 1] : tot) - o;
-            const bool in_stage = staged && pos >= slo && pos + len <= shi;
-            const uint8_t* src = in_stage ? sbase + (pos - sw) : wire + pos;
-            uint8_t* dst = chars + P + o;
-            for (uint64_t k = 0; k < len; ++k) dst[k] = src[k];
+            if (len) {
+                const uint64_t pos = string_pos(a, start, si, rd);
+                const uint8_t* src = in_stage ? lds + sb + (pos - sw) : wire + pos;
+                uint8_t* dst = chars + P + o;
+                for (uint64_t k = 0; k < len; ++k) dst[k] = src[k];
+            }
         }
         ++si;
     }
+    PHASE(5);
+    PHASE_COUNT(6);
+    PHASE_END
 }
 
 __global__ void k_str_offs_zero(VarArgs a) {  // n == 0: str_offs[f][0] = 0
@@ -2177,9 +2209,7 @@ bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total)
     off += round16(p->prefix_len + 16);
     L.stage_cap = round16(static_cast<uint32_t>(cap));
     L.stage_at = off;
-    off += kRtWin + L.stage_cap + 16;  // lds_copy_run may read a dword past a run
-    L.pos_at = off;
-    off += 8 * kBlock * p->nstrings;
+    off += L.stage_cap + 16;  // lds_copy_run may read a dword past a run
     L.len_at = off;
     off += 8 * kBlock * p->nstrings;
     const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
