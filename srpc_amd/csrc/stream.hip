@@ -7,15 +7,15 @@
 // record starts is only known once every record before it was read.  Here
 // the record index is found on the device, then the indexed decode runs.
 //
-// 1. k_stream_scan / k_stream_walk -- the wire is cut into chunks of kChunk
-//    bytes.  A wave per chunk finds the first position p at which a.plaus
-//    records parse one after another (a plausible record start: a string
-//    length read at a wrong offset is almost always past the end of the
-//    wire; see k_stream_scan for the one exception), then a lane per chunk
-//    walks records from there while they start inside the chunk: their
-//    starts, count, the position after them ("exit": the first record start
-//    at or past the chunk end, or where a record failed to parse), and why
-//    the walk stopped.
+// 1. k_stream_chunks -- the wire is cut into chunks of kChunk bytes.  A
+//    lane per chunk (its workgroup's chunks staged in LDS) finds the first
+//    position p at which a.plaus records parse one after another (a
+//    plausible record start: a string length read at a wrong offset is
+//    almost always past the end of the wire; see k_stream_chunks for the one
+//    exception), then walks records from there while they start inside the
+//    chunk: their starts, count, the position after them ("exit": the first
+//    record start at or past the chunk end, or where a record failed to
+//    parse), and why the walk stopped.
 // 2. k_stream_check -- chunk c is right when its start equals the exit of
 //    chunk c - 1 (or chunk c holds no record start at all), chunk 0 when it
 //    starts at 0.  By induction every chunk up to the first wrong one is
@@ -46,7 +46,7 @@
 namespace srpc_impl {
 namespace {
 
-constexpr uint32_t kChunk = 512;    // wire bytes per speculating lane
+constexpr uint32_t kChunk = 64;     // wire bytes per speculating lane
 // records that must parse from a candidate start: with an envelope prefix of
 // 8 bytes or more a wrong start essentially never matches it, so one; else 2
 // (a wrong start that hops onto a true one passes any count: see k_stream_scan)
@@ -84,9 +84,66 @@ __device__ __forceinline__ T ld(const uint8_t* p) {
     return v;
 }
 
+typedef const uint8_t __attribute__((address_space(1))) global_u8;
+typedef uint8_t __attribute__((address_space(3))) lds_u8;
+typedef const uint8_t __attribute__((address_space(3))) lds_u8c;
+typedef const uint32_t __attribute__((address_space(3))) lds_u32c;
+typedef const uint64_t __attribute__((address_space(3))) lds_u64c;
+
+// Wire readers: global memory, or a workgroup's LDS copy of wire bytes
+// [lo, hi) with global memory past it (records that start near the end of the
+// workgroup's span and run past its margin).  Typed address spaces, so the
+// reads are ds_read / global_load, not flat.
+struct GlobalRd {
+    const uint8_t* w;
+    const uint8_t* pre;  // the prefix (device copy)
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const { return ld<uint64_t>(w + p); }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const { return w[p]; }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const { return ld<uint64_t>(pre + i); }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return pre[i]; }
+};
+struct StagedRd {
+    global_u8* w;
+    lds_u8c* lds;  // lds[x] = wire byte base + x, for wire offsets [lo, hi)
+    uint64_t base, lo, hi;
+    lds_u8c* pre;  // LDS copy of the prefix, 8-aligned
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const {
+        if (p >= lo && p + 8 <= hi) {
+            const uint32_t off = static_cast<uint32_t>(p - base);
+            lds_u32c* q = reinterpret_cast<lds_u32c*>(lds + (off & ~3u));
+            const uint32_t sh = off & 3, w0 = q[0], w1 = q[1], w2 = q[2];
+            return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32) |
+                   __builtin_amdgcn_alignbyte(w1, w0, sh);
+        }
+        uint64_t v;
+        __builtin_memcpy(&v, (const uint8_t*)(w + p), 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const { return p >= lo && p < hi ? lds[p - base] : w[p]; }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const { return *reinterpret_cast<lds_u64c*>(pre + i); }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return pre[i]; }
+};
+// The staged bytes only, for speculation: a read past them yields ~0 (no
+// length fits, no prefix matches), so a candidate whose records run past the
+// stage is not plausible -- a start one byte early whose length reads as
+// len * 256 + a char would otherwise send every lane to global memory.  A true
+// start of a record longer than the margin is missed the same way and left to
+// the repair rounds.
+struct StageOnlyRd {
+    StagedRd s;
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const { return p >= s.lo && p + 8 <= s.hi ? s.u64(p) : ~0ull; }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const {
+        return p >= s.lo && p < s.hi ? s.lds[p - s.base] : static_cast<uint8_t>(~s.pre[0]);
+    }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const { return s.pre64(i); }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return s.pre8(i); }
+};
+
 // orc_unpack's cursor over one record at p: the position after it, or p with
 // *err set (SRPC_STATUS_PREFIX / SRPC_STATUS_BOUNDS).
-__device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint32_t* err) {
+template <class Rd>
+__device__ __forceinline__ uint64_t parse_rd(const StreamArgs& a, const Rd& r, uint64_t W, uint64_t p,
+                                             uint32_t* err) {
     *err = 0;
     if (a.prefix_len) {
         if (a.prefix_len > W - p) {
@@ -95,12 +152,12 @@ __device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, 
         }
         uint32_t i = 0;
         for (; i + 8 <= a.prefix_len; i += 8)
-            if (ld<uint64_t>(w + p + i) != ld<uint64_t>(a.prefix + i)) {
+            if (r.u64(p + i) != r.pre64(i)) {
                 *err = SRPC_STATUS_PREFIX;
                 return p;
             }
         for (; i < a.prefix_len; ++i)
-            if (w[p + i] != a.prefix[i]) {
+            if (r.u8(p + i) != r.pre8(i)) {
                 *err = SRPC_STATUS_PREFIX;
                 return p;
             }
@@ -120,7 +177,7 @@ __device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, 
             *err = SRPC_STATUS_BOUNDS;
             return p;
         }
-        const uint64_t len = ld<uint64_t>(w + q);
+        const uint64_t len = r.u64(q);
         q += 8;
         if (len > W - q) {
             *err = SRPC_STATUS_BOUNDS;
@@ -131,14 +188,19 @@ __device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, 
     return q;
 }
 
+__device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint32_t* err) {
+    return parse_rd(a, GlobalRd{w, a.prefix}, W, p, err);
+}
+
 // Walk from p while records start before hi: count, exit, stop reason.
-__device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint64_t hi, uint64_t* cnt,
-                     uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
+template <class Rd>
+__device__ __forceinline__ void walk_rd(const StreamArgs& a, const Rd& r, uint64_t W, uint64_t p, uint64_t hi,
+                                        uint64_t* cnt, uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
     uint64_t k = 0;
     *stop = 0;
     while (p < hi) {
         uint32_t err;
-        const uint64_t q = parse_at(a, w, W, p, &err);
+        const uint64_t q = parse_rd(a, r, W, p, &err);
         if (err) {
             *stop = kStopBad;
             break;
@@ -151,106 +213,178 @@ __device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t
     *cnt = k;
     *exit = p;
 }
+__device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint64_t hi, uint64_t* cnt,
+                     uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
+    walk_rd(a, GlobalRd{w, a.prefix}, W, p, hi, cnt, exit, stop, list, cap);
+}
 
 // Necessary for a record to parse at p: the prefix's first (up to 8) bytes
 // match and the first string's length fits the wire.
-__device__ __forceinline__ bool filter(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p) {
+template <class Rd>
+__device__ __forceinline__ bool filter(const StreamArgs& a, const Rd& r, uint64_t W, uint64_t p) {
     if (a.first_len_at + 8 > W - p) return false;
     if (a.prefix_len) {
         const uint32_t k = a.prefix_len < 8 ? a.prefix_len : 8;
         const uint64_t mask = k == 8 ? ~0ull : (1ull << (8 * k)) - 1;
         uint64_t v = 0;
-        if (8 <= W - p) v = ld<uint64_t>(w + p);
+        if (8 <= W - p) v = r.u64(p);
         else
-            for (uint32_t i = 0; i < k; ++i) v |= static_cast<uint64_t>(w[p + i]) << (8 * i);
+            for (uint32_t i = 0; i < k; ++i) v |= static_cast<uint64_t>(r.u8(p + i)) << (8 * i);
         if (((v ^ a.pre8) & mask) != 0) return false;
     }
-    return ld<uint64_t>(w + p + a.first_len_at) <= W - (p + a.first_len_at + 8);
+    return r.u64(p + a.first_len_at) <= W - (p + a.first_len_at + 8);
 }
 
-__device__ __forceinline__ bool plausible(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p) {
+template <class Rd>
+__device__ __forceinline__ bool plausible(const StreamArgs& a, const Rd& r, uint64_t W, uint64_t p) {
     for (uint32_t k = 0; k < a.plaus; ++k) {
         if (p == W) return k > 0;  // the stream may end right after a record
         uint32_t err;
-        const uint64_t q = parse_at(a, w, W, p, &err);
+        const uint64_t q = parse_rd(a, r, W, p, &err);
         if (err) return false;
         p = q;
     }
     return true;
 }
 
-// Chunk c's speculation, in two kernels.  k_stream_scan (a wave per chunk,
-// its lanes on 64 consecutive candidate positions, so the loads coalesce):
-// the chunk's first plausible record start.  A start 1-3 bytes early is
-// plausible too: its first string length reads the previous record's last
-// chars as low bytes and the true length (little-endian, small) shifted up,
-// and the jump it makes lands on a true record start about once per average
-// record size -- after which every record parses.  So of the plausible starts
-// within the 8 bytes of a length field the one with the smallest first string
-// length is taken: the true start (random strings: 6 % of chunks wrong
-// without this, ~0.05 % with it).  A chunk with no plausible start (inside a
-// long record) passes its entry through: start = exit = kNone, no records.
-__global__ __launch_bounds__(kBlock) void k_stream_scan(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
-                                                        uint64_t C, Chunks ch) {
+// Chunk c's speculation and walk (k_stream_chunks, a lane per chunk of
+// kChunk bytes): a workgroup stages its kBlock chunks plus a margin in LDS
+// (LDS-DMA), and every lane, from LDS, finds its chunk's first plausible
+// record start -- a cheap filter first (the prefix's first bytes, the first
+// string's length fits the wire), then whole records parse from it (a
+// plausible start) -- and walks the records from there that start inside the
+// chunk: their starts, count, the position after them and why the walk
+// stopped.  A start 1-3 bytes early is plausible too: its first string length
+// reads the previous record's last chars as low bytes and the true length
+// (little-endian, small) shifted up, and the jump it makes lands on a true
+// record start about once per average record size -- after which every record
+// parses.  So of the plausible starts within the 8 bytes of a length field the
+// one with the smallest first string length is taken: the true start (random
+// strings: ~0.05 % of chunks wrong).  A chunk with no plausible start (inside
+// a long record) passes its entry through: start = exit = kNone, no records.
+// Reads past the staged bytes (a record running past the margin) go to global
+// memory.  (Round 2 before: a wave per 512-byte chunk speculating and a lane
+// per chunk walking, both from global memory -- chains of dependent reads,
+// 1.7 ms for a 4M-record stream of two strings; a wave per chunk from LDS with
+// a lane-0 walk was compute-bound, profiles/r02_stream_lds_ab.log.)
+constexpr uint32_t kStreamMargin = 2048;
+constexpr uint32_t kStreamStage = kBlock * kChunk + kStreamMargin + 32;
+__global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
+                                                          uint64_t C, Chunks ch) {
+    __shared__ __attribute__((aligned(16))) uint8_t st[kStreamStage + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-    if (c >= C) return;  // wave-uniform
-    const uint64_t lo = c * kChunk, hi = min(lo + kChunk, W);
+    for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
+    const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kBlock;
+    const uint64_t lo = c0 * kChunk;
+    const uint64_t hi = min<uint64_t>(lo + kBlock * kChunk + kStreamMargin, W);
+    const uint64_t A = (reinterpret_cast<uint64_t>(w) + lo) & ~15ull;
+    const uint32_t ng = static_cast<uint32_t>((reinterpret_cast<uint64_t>(w) + hi - A + 15) >> 4);
+    for (uint32_t w0 = threadIdx.x & ~63u; w0 < ng; w0 += kBlock) {
+        const uint32_t gi = w0 + lane;
+        if (gi < ng) {
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(A + 16ull * gi), (lds_u8*)(st + 16 * wb), 16,
+                                             0, 0);
+        }
+    }
+    __syncthreads();  // waits for the LDS-DMA and publishes the stage
+    const StagedRd r{(global_u8*)w, (lds_u8c*)st, A - reinterpret_cast<uint64_t>(w), lo, hi, (lds_u8c*)pre};
+    const StageOnlyRd so{r};
+    const uint64_t c = c0 + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t clo = c * kChunk, chi = min(clo + kChunk, W);
     uint64_t b = kNone;
     if (c == 0) {
         b = 0;  // the stream starts at 0: no speculation
     } else {
-        // a cheap filter at all 512 positions first (the loads of the 8
-        // windows issued together): the prefix's first bytes and the first
-        // string's length; only positions that pass parse whole records
-        uint32_t pass = 0;
+        // the filter at the chunk's 64 positions, from two register windows of
+        // the staged bytes (the first string's length at p + first_len_at, the
+        // prefix's first 8 bytes at p), all lanes in step: a mask of the
+        // positions that pass.  Then the passing positions are parsed in
+        // order until one is plausible -- a lane parses only its few
+        // candidates, instead of the wave running the parse at every position
+        // some lane's filter passed (the divergent per-position loop issued
+        // ~30K instructions per wave).
+        const uint32_t at = static_cast<uint32_t>(clo - r.base);  // LDS offset of the chunk
+        uint64_t mask = 0;
+        {
+            uint32_t d[kChunk / 4 + 3];
+            const uint32_t o = at + a.first_len_at, sh = o & 3;
+            lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)st + (o & ~3u));
 #pragma unroll
-        for (int k = 0; k < static_cast<int>(kChunk / 64); ++k) {
-            const uint64_t p = lo + 64 * k + lane;
-            if (p < hi && filter(a, w, W, p)) pass |= 1u << k;
+            for (int k = 0; k < kChunk / 4 + 3; ++k) d[k] = q[k];
+#pragma unroll
+            for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            // position j: bytes j .. j + 7 of the shifted window
+            // position j passes when len + j <= lim0 = W - (clo + first_len_at + 8)
+            // (a wrapped sum only adds a candidate: the filter stays necessary)
+            const uint64_t need = clo + a.first_len_at + 8;
+            const uint64_t lim0 = need <= W ? W - need : 0;
+#pragma unroll
+            for (int j = 0; j < static_cast<int>(kChunk); ++j) {
+                const int k = j >> 2, s8 = j & 3;
+                const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+                const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+                const uint64_t len = (static_cast<uint64_t>(hi32) << 32) | lo32;
+                mask |= static_cast<uint64_t>(len + j <= lim0) << j;
+            }
+            // positions inside the chunk whose length field lies inside the wire
+            const uint64_t jmax = need <= W ? min<uint64_t>(chi - clo, W - need + 1) : 0;
+            mask &= jmax >= 64 ? ~0ull : (1ull << jmax) - 1;
         }
-        for (int k = 0; k < static_cast<int>(kChunk / 64); ++k) {
-            const uint64_t p = lo + 64 * k + lane;
-            const uint64_t m = __ballot(((pass >> k) & 1) && plausible(a, w, W, p));
-            if (m) {
-                b = lo + 64 * k + __builtin_ctzll(m);
+        if (a.prefix_len && mask) {
+            uint32_t d[kChunk / 4 + 3];
+            const uint32_t sh = at & 3;
+            lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)st + (at & ~3u));
+#pragma unroll
+            for (int k = 0; k < kChunk / 4 + 3; ++k) d[k] = q[k];
+#pragma unroll
+            for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
+            const uint64_t pm = k8 == 8 ? ~0ull : (1ull << (8 * k8)) - 1;
+            uint64_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < static_cast<int>(kChunk); ++j) {
+                const int k = j >> 2, s8 = j & 3;
+                const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+                const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+                const uint64_t v = (static_cast<uint64_t>(hi32) << 32) | lo32;
+                keep |= static_cast<uint64_t>(((v ^ a.pre8) & pm) == 0) << j;
+            }
+            mask &= keep;
+        }
+        const uint64_t passing = mask;
+        while (mask) {
+            const uint32_t j = __builtin_ctzll(mask);
+            if (plausible(a, so, W, clo + j)) {
+                b = clo + j;
                 break;
             }
+            mask &= mask - 1;
         }
         if (b != kNone) {
-            // candidates b .. b + 7: argmin of (first string length, position)
-            const uint64_t q = b + lane;
-            bool cand = lane < 8 && q < hi && a.first_len_at + 8 <= W - q;
-            uint64_t l = cand ? ld<uint64_t>(w + q + a.first_len_at) : ~0ull;
-            if (cand && lane > 0 && !plausible(a, w, W, q)) cand = false;
-            uint64_t kl = cand ? l : ~0ull;
-            uint32_t ki = cand ? lane : 64u;
-            for (int d = 32; d > 0; d >>= 1) {
-                const uint64_t ol = __shfl_xor(kl, d, 64);
-                const uint32_t oi = __shfl_xor(ki, d, 64);
-                if (ol < kl || (ol == kl && oi < ki)) {
-                    kl = ol;
-                    ki = oi;
+            // candidates b .. b + 7 inside the chunk (filter-passing, plausible):
+            // argmin of (first string length, position)
+            const uint32_t jb = static_cast<uint32_t>(b - clo);
+            uint64_t cand = (passing >> (jb + 1)) & 0x7f;
+            uint64_t best = so.u64(b + a.first_len_at), pick = b;
+            while (cand) {
+                const uint64_t q = b + 1 + __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const uint64_t l = so.u64(q + a.first_len_at);
+                if (l < best && plausible(a, so, W, q)) {
+                    best = l;
+                    pick = q;
                 }
             }
-            b += ki;  // lane 0 (b itself) is always a candidate
+            b = pick;
         }
     }
-    if (lane == 0) ch.start[c] = b;
-}
-
-// k_stream_walk (a lane per chunk): the records from the chunk's start that
-// start inside the chunk -- their starts, count, the position after them and
-// why the walk stopped.
-__global__ __launch_bounds__(kBlock) void k_stream_walk(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
-                                                        uint64_t C, Chunks ch) {
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= C) return;
-    const uint64_t hi = min((c + 1) * kChunk, W);
-    const uint64_t b = ch.start[c];
     uint64_t cnt = 0, exit = kNone;
     uint32_t stop = 0;
-    if (b != kNone) walk(a, w, W, b, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
+    if (b != kNone) walk_rd(a, r, W, b, chi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
+    ch.start[c] = b;
     ch.cnt[c] = cnt;
     ch.exit[c] = exit;
     ch.stop[c] = stop;
@@ -558,10 +692,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     launch(k_stream_ctl_reset, dim3(static_cast<uint32_t>(std::min<uint64_t>((nblk + 255) / 256 + 1, 1024))),
            dim3(256), 0, s, ch, nblk);
     if (wire_len) {
-        const uint64_t gw = (C + kBlock / 64 - 1) / (kBlock / 64);
-        if (gw > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-        launch(k_stream_scan, dim3(static_cast<uint32_t>(gw)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
-        launch(k_stream_walk, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+        launch(k_stream_chunks, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
         launch(k_stream_check, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
         for (int r = 0; r < kRepairRounds; ++r) {  // gated: no-ops once every chunk agrees
             launch(k_stream_refix, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
