@@ -169,15 +169,15 @@ def test_random_schemas_vs_oracle(n, schema):
 
 @pytest.mark.parametrize("n", [1, 3, 5, 4097, 65539])
 @pytest.mark.parametrize("kinds,prefix", [
-    ([oracle.INT16, oracle.INT64], b"abc"),  # 13 B, G = 4, prefix bytes inside a group's dwords
-    ([oracle.INT64, oracle.INT64, oracle.INT64, oracle.INT32, oracle.INT8], b""),  # 29 B, 32-byte column loads
+    ([oracle.INT16, oracle.INT64], b"abc"),  # 13 B, prefix bytes between fields of odd offsets
+    ([oracle.INT64, oracle.INT64, oracle.INT64, oracle.INT32, oracle.INT8], b""),  # 29 B
     ([oracle.INT8, oracle.INT16, oracle.INT8, oracle.INT32, oracle.INT8, oracle.INT64], b"\x01\x02"),  # 19 B
-    ([oracle.INT16, oracle.INT32], b"q" * 24),  # 30 B, G = 2, mostly prefix
+    ([oracle.INT16, oracle.INT32], b"q" * 24),  # 30 B, mostly prefix
 ])
-def test_odd_stride_register_groups_vs_oracle(n, kinds, prefix):
-    """Small records whose stride is not a multiple of 4 (the TILE pack's
-    register-assembled groups): sizes that leave a partial last group, a
-    partial last tile and a ragged wire tail, with and without an envelope."""
+def test_odd_stride_records_vs_oracle(n, kinds, prefix):
+    """Small TILE records whose stride is not a multiple of 4 (2/4/8-byte
+    values at odd image offsets): sizes that leave a partial last tile and a
+    ragged wire tail, with and without an envelope."""
     rng = np.random.default_rng(n * 7 + len(kinds) + len(prefix))
     cols = [rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(oracle.KIND_DTYPE[k])
             for k in kinds]
@@ -535,6 +535,39 @@ def test_strings_random_vs_oracle(n, schema, maxlen, envelope, vk):
         assert back[f].tobytes() == ocols[f].tobytes(), f
         if k == oracle.STRING:
             assert np.array_equal(boffs[f], ooffs[f])
+
+
+@pytest.mark.parametrize("schema,maxlen,envelope", [("mixed", 64, None), ("two_str", 32, "request")])
+def test_strings_many_tiles_vs_oracle(schema, maxlen, envelope):
+    """More 256-record tiles than the device holds workgroups (records of
+    >= 40 bytes: the pack's resident grid loops over its tiles, each
+    workgroup several times), byte for byte against the oracle; the stream
+    decode of the same wire rebuilds the index."""
+    kinds = {"mixed": [oracle.INT8, oracle.STRING, oracle.INT64, oracle.BOOL, oracle.STRING, oracle.INT16],
+             "two_str": [oracle.STRING, oracle.INT32, oracle.STRING]}[schema]
+    n = 700_001  # 2735 tiles
+    rng = np.random.default_rng(7)
+    cols, offs = _random_string_batch(kinds, n, rng, maxlen)
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker.for_request(sch, "Svc_servicer::m") if envelope else GpuPacker(sch)
+    want = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    assert len(want) // n >= 40  # the looping pack
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st[0] == 0 and wire == want
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
+    back, boffs, st = gpu_unpack_var(p, kinds, want, n, rec)
+    assert st[0] == 0
+    for f, k in enumerate(kinds):
+        if k == oracle.STRING:
+            assert np.array_equal(boffs[f], offs[f] - offs[f][0])
+            assert back[f].tobytes() == cols[f][:int(offs[f][n])].tobytes(), f
+        else:
+            assert back[f].tobytes() == cols[f].tobytes(), f
+    from tests.test_gpu_stream import stream_unpack
+    sback, sboffs, srec, sst = stream_unpack(p, kinds, want, n)
+    assert sst == (0, 2**64 - 1) and np.array_equal(srec, rec)
+    for f in range(len(kinds)):
+        assert sback[f].tobytes() == back[f].tobytes(), f
 
 
 @pytest.mark.parametrize("maxlens", [(0, 700), (3, 0, 900), (700, 2, 40), (0, 0)])
