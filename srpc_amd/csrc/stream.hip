@@ -16,7 +16,8 @@
 //    chunk: their starts, count, the position after them ("exit": the first
 //    record start at or past the chunk end, or where a record failed to
 //    parse), and why the walk stopped.
-// 2. k_stream_check -- chunk c is right when its start equals the exit of
+// 2. the check (in k_stream_chunks; k_stream_check_edges for each
+//    workgroup's leading chunks) -- chunk c is right when its start equals the exit of
 //    chunk c - 1 (or chunk c holds no record start at all), chunk 0 when it
 //    starts at 0.  By induction every chunk up to the first wrong one is
 //    right.
@@ -247,6 +248,38 @@ __device__ __forceinline__ bool plausible(const StreamArgs& a, const Rd& r, uint
     return true;
 }
 
+// The entry of chunk c (the first record start at or after its beginning):
+// the exit of the nearest chunk before it with a record start, or a stop.
+__device__ __forceinline__ uint64_t entry_of(const Chunks& ch, uint64_t c, bool* stopped) {
+    *stopped = false;
+    for (uint64_t j = c; j-- > 0;) {
+        if (ch.start[j] == kNone) continue;  // passes its own entry through
+        *stopped = ch.stop[j] != 0;
+        return ch.exit[j];
+    }
+    return 0;  // unreachable: chunk 0 always starts at 0
+}
+
+// Chunk c agrees with its entry e when it starts exactly there, or -- e past
+// the chunk's end -- when it found no record start.
+__device__ __forceinline__ bool agrees(uint64_t e, uint64_t chunk_hi, uint64_t start) {
+    return e >= chunk_hi ? start == kNone : start == e;
+}
+
+// A wave's bad chunks: one atomic per wave on the flags (every lane of the
+// wave calls this: thousands of bad chunks on one control word serialised the
+// check kernel), one per 256-chunk block word.
+__device__ __forceinline__ void note_bad(const Chunks& ch, uint64_t c, bool bad, int any_at, int first_at) {
+    const uint64_t m = __ballot(bad);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+    if (lane == lead) {  // the wave's first bad chunk; a wave's 64 chunks share one block word
+        atomicOr(&ch.ctl[any_at], 1u);
+        atomicMin(&ch.ctl[first_at], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
+        atomicOr(&ch.blk[c >> 8], 1u);
+    }
+}
+
 // Chunk c's speculation and walk (k_stream_chunks, a lane per chunk of
 // kChunk bytes): a workgroup stages its kBlock chunks plus a margin in LDS
 // (LDS-DMA), and every lane, from LDS, finds its chunk's first plausible
@@ -292,10 +325,11 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
     const StagedRd r{(global_u8*)w, (lds_u8c*)st, A - reinterpret_cast<uint64_t>(w), lo, hi, (lds_u8c*)pre};
     const StageOnlyRd so{r};
     const uint64_t c = c0 + threadIdx.x;
-    if (c >= C) return;
     const uint64_t clo = c * kChunk, chi = min(clo + kChunk, W);
     uint64_t b = kNone;
-    if (c == 0) {
+    if (c >= C) {
+        // past the last chunk: nothing (the check below still needs the lane)
+    } else if (c == 0) {
         b = 0;  // the stream starts at 0: no speculation
     } else {
         // the filter at the chunk's 64 positions, from two register windows of
@@ -384,59 +418,55 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
     uint64_t cnt = 0, exit = kNone;
     uint32_t stop = 0;
     if (b != kNone) walk_rd(a, r, W, b, chi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
-    ch.start[c] = b;
-    ch.cnt[c] = cnt;
-    ch.exit[c] = exit;
-    ch.stop[c] = stop;
-    if (stop) atomicOr(&ch.blk[c >> 8], 2u);
-}
-
-// The entry of chunk c (the first record start at or after its beginning):
-// the exit of the nearest chunk before it with a record start, or a stop.
-__device__ __forceinline__ uint64_t entry_of(const Chunks& ch, uint64_t c, bool* stopped) {
-    *stopped = false;
-    for (uint64_t j = c; j-- > 0;) {
-        if (ch.start[j] == kNone) continue;  // passes its own entry through
-        *stopped = ch.stop[j] != 0;
-        return ch.exit[j];
+    __shared__ uint64_t s_start[kBlock], s_exit[kBlock];
+    __shared__ uint32_t s_stop[kBlock];
+    s_start[threadIdx.x] = b;
+    s_exit[threadIdx.x] = exit;
+    s_stop[threadIdx.x] = stop;
+    if (c < C) {
+        ch.start[c] = b;
+        ch.cnt[c] = cnt;
+        ch.exit[c] = exit;
+        ch.stop[c] = stop;
+        if (stop) atomicOr(&ch.blk[c >> 8], 2u);
     }
-    return 0;  // unreachable: chunk 0 always starts at 0
-}
-
-// Chunk c agrees with its entry e when it starts exactly there, or -- e past
-// the chunk's end -- when it found no record start.
-__device__ __forceinline__ bool agrees(uint64_t e, uint64_t chunk_hi, uint64_t start) {
-    return e >= chunk_hi ? start == kNone : start == e;
-}
-
-// A wave's bad chunks: one atomic per wave on the flags (every lane of the
-// wave calls this: thousands of bad chunks on one control word serialised the
-// check kernel), one per 256-chunk block word.
-__device__ __forceinline__ void note_bad(const Chunks& ch, uint64_t c, bool bad, int any_at, int first_at) {
-    const uint64_t m = __ballot(bad);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
-    if (lane == lead) {  // the wave's first bad chunk; a wave's 64 chunks share one block word
-        atomicOr(&ch.ctl[any_at], 1u);
-        atomicMin(&ch.ctl[first_at], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
-        atomicOr(&ch.blk[c >> 8], 1u);
+    __syncthreads();
+    // the check (k_stream_check's rule) for chunks whose entry comes from a
+    // chunk of this workgroup; the others -- the leading chunks up to the
+    // first one with a record start -- are checked by k_stream_check_edges
+    bool bad = false;
+    if (c < C && c > 0) {
+        int j = static_cast<int>(threadIdx.x) - 1;
+        while (j >= 0 && s_start[j] == kNone) --j;  // chunks with no start pass their entry through
+        if (j >= 0) bad = !(s_stop[j] != 0 || agrees(s_exit[j], chi, b));
     }
+    if (c < C && (c == 0 || threadIdx.x > 0)) {
+        bool edge = c > 0;
+        for (int j = static_cast<int>(threadIdx.x) - 1; edge && j >= 0; --j) edge = s_start[j] == kNone;
+        if (!edge) ch.bad[c] = bad ? 1u : 0u;
+    }
+    note_bad(ch, c, bad, 0, 2);
 }
 
-__global__ __launch_bounds__(kBlock) void k_stream_check(uint64_t W, uint64_t C, Chunks ch) {
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c == 0 && C) ch.bad[0] = 0;
-    if (c >= C || c == 0) {
-        note_bad(ch, c, false, 0, 2);
-        return;
+// The leading chunks of every workgroup of k_stream_chunks (those before and
+// including its first chunk with a record start), whose entry is the exit of
+// an earlier workgroup's chunk: a lane per workgroup, k_stream_check's rule.
+__global__ __launch_bounds__(kBlock) void k_stream_check_edges(uint64_t W, uint64_t C, Chunks ch) {
+    const uint64_t wg = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x + 1;  // workgroup 0 needs none
+    if (wg * kBlock >= C) return;
+    for (uint64_t c = wg * kBlock; c < C && c < (wg + 1) * kBlock; ++c) {
+        const uint64_t hi = min((c + 1) * kChunk, W);
+        bool stopped;
+        const uint64_t e = entry_of(ch, c, &stopped);
+        const bool ok = stopped || agrees(e, hi, ch.start[c]);
+        ch.bad[c] = ok ? 0u : 1u;
+        if (!ok) {
+            atomicOr(&ch.ctl[0], 1u);
+            atomicMin(&ch.ctl[2], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
+            atomicOr(&ch.blk[c >> 8], 1u);
+        }
+        if (ch.start[c] != kNone) break;  // later chunks of the workgroup were checked in k_stream_chunks
     }
-    const uint64_t hi = min((c + 1) * kChunk, W);
-    bool stopped;
-    const uint64_t e = entry_of(ch, c, &stopped);
-    // after a stop nothing counts (masked later); otherwise start must agree
-    const bool ok = stopped || agrees(e, hi, ch.start[c]);
-    ch.bad[c] = ok ? 0u : 1u;
-    note_bad(ch, c, !ok, 0, 2);
 }
 
 // Parallel repair rounds (before the serial fixer): every bad chunk walks
@@ -448,45 +478,55 @@ __global__ __launch_bounds__(kBlock) void k_stream_check(uint64_t W, uint64_t C,
 __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
                                                          uint64_t C, Chunks ch) {
     if (ch.ctl[0] == 0) return;
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= C || !ch.bad[c]) return;
-    // only a chunk whose entry is final: no bad chunk between it and the chunk
-    // that provides its entry (a chunk marked bad only because its
-    // predecessor was wrong keeps its own, probably right, speculation)
-    for (uint64_t j = c; j-- > 0;) {
-        if (ch.bad[j]) return;
-        if (ch.start[j] != kNone) break;
+    // grid-stride (a small grid: the launch is a no-op whenever every chunk agrees)
+    for (uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; c < C;
+         c += static_cast<uint64_t>(gridDim.x) * kBlock) {
+        if (!ch.bad[c]) continue;
+        // only a chunk whose entry is final: no bad chunk between it and the chunk
+        // that provides its entry (a chunk marked bad only because its
+        // predecessor was wrong keeps its own, probably right, speculation)
+        bool final_entry = true;
+        for (uint64_t j = c; j-- > 0;) {
+            if (ch.bad[j]) {
+                final_entry = false;
+                break;
+            }
+            if (ch.start[j] != kNone) break;
+        }
+        if (!final_entry) continue;
+        const uint64_t hi = min((c + 1) * kChunk, W);
+        bool stopped;
+        const uint64_t e = entry_of(ch, c, &stopped);
+        if (stopped) continue;
+        uint64_t cnt = 0, exit = kNone, start = kNone;
+        uint32_t stop = 0;
+        if (e < hi) {
+            start = e;
+            walk(a, w, W, e, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
+        }
+        ch.start[c] = start;
+        ch.cnt[c] = cnt;
+        ch.exit[c] = exit;
+        ch.stop[c] = stop;
+        if (stop) atomicOr(&ch.blk[c >> 8], 2u);
     }
-    const uint64_t hi = min((c + 1) * kChunk, W);
-    bool stopped;
-    const uint64_t e = entry_of(ch, c, &stopped);
-    if (stopped) return;
-    uint64_t cnt = 0, exit = kNone, start = kNone;
-    uint32_t stop = 0;
-    if (e < hi) {
-        start = e;
-        walk(a, w, W, e, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
-    }
-    ch.start[c] = start;
-    ch.cnt[c] = cnt;
-    ch.exit[c] = exit;
-    ch.stop[c] = stop;
-    if (stop) atomicOr(&ch.blk[c >> 8], 2u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t C, Chunks ch) {
     if (ch.ctl[0] == 0) return;
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= C || c == 0) {
-        note_bad(ch, c, false, 3, 4);
-        return;
+    // grid-stride, whole waves per step (note_bad ballots over the wave)
+    for (uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kBlock; c0 < C; c0 += static_cast<uint64_t>(gridDim.x) * kBlock) {
+        const uint64_t c = c0 + threadIdx.x;
+        bool ok = true;
+        if (c < C && c > 0) {
+            const uint64_t hi = min((c + 1) * kChunk, W);
+            bool stopped;
+            const uint64_t e = entry_of(ch, c, &stopped);
+            ok = stopped || agrees(e, hi, ch.start[c]);
+            ch.bad[c] = ok ? 0u : 1u;
+        }
+        note_bad(ch, c, !ok, 3, 4);
     }
-    const uint64_t hi = min((c + 1) * kChunk, W);
-    bool stopped;
-    const uint64_t e = entry_of(ch, c, &stopped);
-    const bool ok = stopped || agrees(e, hi, ch.start[c]);
-    ch.bad[c] = ok ? 0u : 1u;
-    note_bad(ch, c, !ok, 3, 4);
 }
 
 __global__ void k_stream_round_end(Chunks ch) {
@@ -693,10 +733,12 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
            dim3(256), 0, s, ch, nblk);
     if (wire_len) {
         launch(k_stream_chunks, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
-        launch(k_stream_check, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
+        const uint64_t ge = (g + kBlock - 1) / kBlock;  // a lane per workgroup of k_stream_chunks
+        launch(k_stream_check_edges, dim3(static_cast<uint32_t>(ge)), dim3(kBlock), 0, s, wire_len, C, ch);
+        const uint32_t gr = static_cast<uint32_t>(std::min<uint64_t>(g, 2048));
         for (int r = 0; r < kRepairRounds; ++r) {  // gated: no-ops once every chunk agrees
-            launch(k_stream_refix, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
-            launch(k_stream_recheck, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, wire_len, C, ch);
+            launch(k_stream_refix, dim3(gr), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
+            launch(k_stream_recheck, dim3(gr), dim3(kBlock), 0, s, wire_len, C, ch);
             launch(k_stream_round_end, dim3(1), dim3(64), 0, s, ch);
         }
         launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
