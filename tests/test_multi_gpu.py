@@ -37,3 +37,56 @@ def test_native_comm_python_one_rank():
     torch.cuda.synchronize()
     assert torch.equal(out, local)
     c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("n", [17, 4099, 100_003])
+def test_shards_concatenate_to_the_batch(world, n):
+    """The reference appends records to one buffer (core.hpp:34, packer.hpp:73),
+    so the wire of a batch is the concatenation of its shards' wires: every
+    rank's srpc_shard_range slice (16-record aligned cuts) packed on its own --
+    here all on device 0 -- and laid end to end equals the oracle's batch,
+    for fixed records (Quad) and for string records (offsets sliced, chars
+    shared: each shard's offsets start wherever its first record's chars do)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import numpy as np
+
+    import oracle
+    from srpc_amd import QUAD, GpuPacker, Schema
+    from srpc_amd.shard import native_shard_range
+    from tests.test_gpu_parity import _dev_u64, _random_string_batch, dev, empty, host
+
+    cols = oracle.splitmix_columns_i32(4, n)
+    p = GpuPacker(QUAD)
+    dcols = [dev(c) for c in cols]
+    parts = []
+    for r in range(world):
+        lo, hi = native_shard_range(n, r, world)
+        assert lo % 16 == 0 and (hi % 16 == 0 or hi == n)
+        w = empty(16 * (hi - lo) + 16)
+        if hi > lo:
+            p.pack([c[4 * lo:4 * hi] for c in dcols], hi - lo, w)
+        parts.append(host(w, 16 * (hi - lo)).tobytes())
+    assert b"".join(parts) == oracle.pack([oracle.INT32] * 4, cols, n)
+
+    kinds = [oracle.INT8, oracle.STRING, oracle.INT64]
+    scols, soffs = _random_string_batch(kinds, n, np.random.default_rng(n + world), 40)
+    sp = GpuPacker(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    want = oracle.pack(kinds, scols, n, b"", list(soffs))
+    dc = [dev(scols[0]), dev(scols[1]), dev(scols[2])]
+    doff = _dev_u64(soffs[1])
+    parts = []
+    for r in range(world):
+        lo, hi = native_shard_range(n, r, world)
+        m = hi - lo
+        total = 17 * m + int(soffs[1][hi] - soffs[1][lo])
+        w, rec = empty(total + 16), empty(8 * (m + 1))
+        sb = sp.var_scratch_bytes(m, total)
+        scratch = empty(sb + 16)
+        if m:
+            sp.pack_var([dc[0][lo:hi], dc[1], dc[2][8 * lo:8 * hi]], [None, doff[8 * lo:8 * (hi + 1)], None], m, w,
+                        total, rec, scratch, sb)
+        parts.append(host(w, total).tobytes())
+    assert b"".join(parts) == want
