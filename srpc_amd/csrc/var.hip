@@ -1330,15 +1330,19 @@ __global__ __launch_bounds__(kBlock) void k_pack_var_rt_loop(VarArgs a, RtArgs L
     }
 }
 
-// One tile per workgroup (records under kRtPersistMin bytes on average: the
-// loop kernel's per-tile barriers and wider register state cost more than
-// its overlap saves on 4-8 KiB tiles, profiles/r02_var_rt_persist_ab.log).
+// One tile of kBlock * RPL records per workgroup (records under kRtPersistMin
+// bytes on average: the loop kernel's per-tile barriers and wider register
+// state cost more than its overlap saves on 4-8 KiB tiles,
+// profiles/r02_var_rt_persist_ab.log); lane i owns records i, i + kBlock, ...
+// -- RPL > 1 makes a short-record tile as large as a long-record one.
+template <int RPL>
 __global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uint64_t n, uint8_t* __restrict__ wire,
                                                         uint64_t wire_cap, uint64_t* __restrict__ rec_offs,
                                                         srpc_unpack_status* st) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ RtRegion rt[kRtRegions];
-    __shared__ uint64_t lofs[kBlock + 1];     // local record starts (image positions minus h), [nr] = total
+    constexpr uint32_t kTR = kBlock * RPL;   // records per tile
+    __shared__ uint64_t lofs[kTR + 1];        // local record starts (image positions minus h), [nr] = total
     __shared__ uint64_t climit[kMaxFields];   // string field: soff[f][n] (end of its chars)
     __shared__ uint32_t fsw[kMaxFields];      // string ordinal -> LDS offset of its window entry 0
     __shared__ uint32_t fch[kMaxFields];      // string ordinal -> LDS offset of char soff[f][r0]
@@ -1351,8 +1355,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uin
     for (uint32_t i = threadIdx.x; i < a.prefix_len + 32; i += kBlock)
         lds[L.pre_at + i] = i < a.prefix_len ? a.prefix[i] : 0;
     for (uint32_t f = threadIdx.x; f < a.nfields; f += kBlock) climit[f] = a.size[f] ? 0 : a.soff[f][n];
-    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * kBlock;
-    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kBlock, n - r0));
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * kTR;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(kTR, n - r0));
     // 1. staging table (wave 0, one lane per region): region g's granules
     // land in the stage in granule order, granule x at stage_at + 16 x
     if (threadIdx.x < 64) {
@@ -1430,31 +1434,41 @@ __global__ __launch_bounds__(kBlock) void k_pack_var_rt(VarArgs a, RtArgs L, uin
     }
     __syncthreads();  // waits for the LDS-DMA (vmcnt(0)) and publishes the stage
     // 3. record starts from the staged offsets windows
-    const uint32_t i = threadIdx.x;
-    if (i < nr) {
-        uint64_t e = static_cast<uint64_t>(i + 1) * a.fixed_bytes;
-        for (uint32_t si = 0; si < ns; ++si) {
-            const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + fsw[si]);
-            e += w[i + 1] - w[0];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const uint32_t i = threadIdx.x + q * kBlock;
+        if (i < nr) {
+            uint64_t e = static_cast<uint64_t>(i + 1) * a.fixed_bytes;
+            for (uint32_t si = 0; si < ns; ++si) {
+                const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + fsw[si]);
+                e += w[i + 1] - w[0];
+            }
+            lofs[i + 1] = e;
         }
-        lofs[i + 1] = e;
     }
-    if (i == 0) lofs[0] = 0;
+    if (threadIdx.x == 0) lofs[0] = 0;
     __syncthreads();
     const uint64_t base = s_base, total = lofs[nr];
-    if (i < nr) {
-        const uint64_t start = base + lofs[i], end = base + lofs[i + 1];
-        rec_offs[r0 + i] = start;
-        if (st && start <= wire_cap && wire_cap < end) report_bad(st, SRPC_STATUS_BOUNDS, r0 + i);
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const uint32_t i = threadIdx.x + q * kBlock;
+        if (i < nr) {
+            const uint64_t start = base + lofs[i], end = base + lofs[i + 1];
+            rec_offs[r0 + i] = start;
+            if (st && start <= wire_cap && wire_cap < end) report_bad(st, SRPC_STATUS_BOUNDS, r0 + i);
+        }
     }
-    if (i == 0 && r0 + nr == n) rec_offs[n] = base + total;
+    if (threadIdx.x == 0 && r0 + nr == n) rec_offs[n] = base + total;
     const uint32_t h = static_cast<uint32_t>(base & 15);
     const uint64_t gbase = base & ~15ull;
     const uint64_t wend = min(base + total, wire_cap);  // wire bytes of this tile end here
     uint8_t* img = lds + L.img_at;
     if (s_fits && h + total <= L.img_cap) {
         // 4. records -> LDS image
-        if (i < nr) {
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const uint32_t i = threadIdx.x + q * kBlock;
+            if (i >= nr) break;
             uint32_t d = L.img_at + h + static_cast<uint32_t>(lofs[i]);
             if (a.prefix_len) {
                 lds_copy_run(lds, d, L.pre_at, a.prefix_len);
@@ -2149,6 +2163,7 @@ uint32_t round16(uint32_t b) { return (b + 15) & ~15u; }
 #define SRPC_RT_PERSIST_MIN 40
 #endif
 constexpr uint64_t kRtPersistMin = SRPC_RT_PERSIST_MIN;
+constexpr uint64_t kRtTwoPerLane = 20;
 template <typename K>
 uint64_t resident_grid(K kernel, uint32_t lds, int device) {
     int per_cu = 0, cus = 0;
@@ -2167,25 +2182,26 @@ uint64_t resident_grid(K kernel, uint32_t lds, int device) {
 // fixes it (SRPC_TUNE_VAR_IMAGE_BYTES); the stage holds the tile's offsets
 // windows and column slices plus the chars that such a span can hold.  Tiles
 // that do not fit take the chunk walk.
-RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total) {
+RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total, uint32_t rpl = 1) {
     RtArgs L{};
+    const uint32_t tr = kBlock * rpl;  // records per tile
     uint32_t off = 0;
     L.pre_at = off;
     off += round16(p->prefix_len + 32);
     uint64_t img = p->rt_img_cap;
     if (!img) {
-        img = std::min<uint64_t>(avg, kRtImageMax) * kBlock;
+        img = std::min<uint64_t>(avg, kRtImageMax) * tr;
         img = std::min<uint64_t>(std::max<uint64_t>(img + img / 16 + 64, kRtImageMin), kRtImageMax);
     }
     L.img_cap = round16(static_cast<uint32_t>(img));
     uint64_t chars = p->rt_ch_cap;
     if (p->rt_ch_cap_auto) {
-        const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
+        const uint64_t fixed_span = static_cast<uint64_t>(tr) * p->fixed_bytes;
         chars = L.img_cap > fixed_span ? L.img_cap - fixed_span : 0;
     }
-    uint32_t fixed = p->nstrings * kRtWin;
+    uint32_t fixed = p->nstrings * (((tr + 1) * 8 + 16 + 15) & ~15u);  // offsets windows
     for (uint32_t f = 0; f < p->nfields; ++f)
-        if (p->size[f]) fixed += round16(kBlock * p->size[f] + 16);
+        if (p->size[f]) fixed += round16(tr * p->size[f] + 16);
     L.stage_cap = fixed + round16(static_cast<uint32_t>(chars)) + 16 * p->nstrings;
     L.stage_at = off;
     off += L.stage_cap + 16;  // lds_copy_run may read a dword past a chars run
@@ -2289,7 +2305,11 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
         if (!wire) return SRPC_E_INVALID;
         uint32_t lds = 0;
         const bool loop = wire_cap / n >= kRtPersistMin;
-        const RtArgs R = rt_layout(p, wire_cap / n, &lds);
+        // records under kRtTwoPerLane bytes on average: two per lane (a tile of
+        // 512 records; 0-16 B strings 114 -> 98 us, but 0-32 B 67 -> 79 us and
+        // four per lane slower on both, profiles/r02_var_rt_rpl_ab.log)
+        const uint32_t rpl = !loop && wire_cap / n < kRtTwoPerLane ? 2 : 1;
+        const RtArgs R = rt_layout(p, wire_cap / n, &lds, rpl);
         // records of >= SRPC_RT_PERSIST_MIN bytes on average: resident workgroups
         // only, each looping over its tiles with the next tile's loads in flight
         // (two strings + request envelope 228 -> 193 us, 0-64 B 134 -> 127 us);
@@ -2301,8 +2321,13 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
             launch(k_pack_var_rt_loop, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), lds, s, a, R, n, wire,
                    wire_cap, rec_offs, st);
         } else {
-            launch(k_pack_var_rt, dim3(static_cast<uint32_t>(ntiles)), dim3(kBlock), lds, s, a, R, n, wire,
-                   wire_cap, rec_offs, st);
+            const uint64_t tiles = (n + kBlock * rpl - 1) / (kBlock * rpl);
+            if (rpl == 2)
+                launch(k_pack_var_rt<2>, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), lds, s, a, R, n, wire,
+                       wire_cap, rec_offs, st);
+            else
+                launch(k_pack_var_rt<1>, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), lds, s, a, R, n, wire,
+                       wire_cap, rec_offs, st);
         }
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }

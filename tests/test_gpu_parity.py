@@ -499,7 +499,7 @@ def _random_string_batch(kinds, n, rng, maxlen):
 
 @pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 2047, 2048, 2049, 30_001])
 @pytest.mark.parametrize("schema,maxlen,envelope", [
-    ("s", 40, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
+    ("s", 40, None), ("s", 16, None), ("mixed", 300, None), ("two_str", 16, "request"), ("s", 5000, None),
     ("nested", 64, "response"), ("wide", 24, "request")])
 @pytest.mark.parametrize("vk", [None, 0, 2], ids=["default", "walk", "tiles"])
 def test_strings_random_vs_oracle(n, schema, maxlen, envelope, vk):
