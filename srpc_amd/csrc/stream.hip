@@ -74,7 +74,7 @@ struct Chunks {      // per chunk (scratch, C entries each)
     uint32_t* bad;    // chunk disagrees with its predecessor
     uint32_t* blk;    // per 256 chunks: bit 0 some chunk is bad, bit 1 some chunk stops
     uint32_t* ctl;    // [0] any bad, [1] the stream's stop chunk, [2] the first bad chunk, [3..6] see below
-    uint64_t* list;   // per chunk: the starts of its records, cap entries each
+    uint8_t* list;    // per chunk: its records' starts minus the chunk's first byte, cap entries each
     uint32_t cap;     // 1 + kChunk / the smallest record (fixed_bytes): a chunk's records at most
 };
 
@@ -196,7 +196,7 @@ __device__ uint64_t parse_at(const StreamArgs& a, const uint8_t* w, uint64_t W, 
 // Walk from p while records start before hi: count, exit, stop reason.
 template <class Rd>
 __device__ __forceinline__ void walk_rd(const StreamArgs& a, const Rd& r, uint64_t W, uint64_t p, uint64_t hi,
-                                        uint64_t* cnt, uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
+                                        uint64_t* cnt, uint64_t* exit, uint32_t* stop, uint8_t* list, uint32_t cap) {
     uint64_t k = 0;
     *stop = 0;
     while (p < hi) {
@@ -206,7 +206,8 @@ __device__ __forceinline__ void walk_rd(const StreamArgs& a, const Rd& r, uint64
             *stop = kStopBad;
             break;
         }
-        if (k < cap) list[k] = p;  // always: records are >= fixed_bytes long
+        // always: records are >= fixed_bytes long; a start lies in [chunk, chunk + kChunk)
+        if (k < cap) list[k] = static_cast<uint8_t>(p % kChunk);
         ++k;
         p = q;
     }
@@ -215,7 +216,7 @@ __device__ __forceinline__ void walk_rd(const StreamArgs& a, const Rd& r, uint64
     *exit = p;
 }
 __device__ void walk(const StreamArgs& a, const uint8_t* w, uint64_t W, uint64_t p, uint64_t hi, uint64_t* cnt,
-                     uint64_t* exit, uint32_t* stop, uint64_t* list, uint32_t cap) {
+                     uint64_t* exit, uint32_t* stop, uint8_t* list, uint32_t cap) {
     walk_rd(a, GlobalRd{w, a.prefix}, W, p, hi, cnt, exit, stop, list, cap);
 }
 
@@ -600,9 +601,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, 
     if (c >= C || counts[c] == 0) return;
     const uint64_t r0 = recbase[c];
     if (r0 > n) return;
-    const uint64_t* list = ch.list + c * ch.cap;
+    const uint8_t* list = ch.list + c * ch.cap;
     const uint64_t k1 = min<uint64_t>(counts[c], n - r0 + 1);  // [n]: the start of record n, if any
-    for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = list[k];
+    for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = c * kChunk + list[k];
 }
 
 // Records the stream holds: T = sum of counts.  rec_offs[T] = where the stream
@@ -675,7 +676,7 @@ StreamLayout stream_layout(uint64_t wire_len, uint32_t fixed_bytes) {
     o += r256(8 * (xscan_parts(L.C) + 1));
     L.cap = 1 + kChunk / std::max<uint32_t>(fixed_bytes, 1);
     L.list = o;
-    o += r256(8 * L.C * L.cap);
+    o += r256(L.C * L.cap);  // one byte per start
     L.total = o;
     return L;
 }
@@ -711,7 +712,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     Chunks ch{reinterpret_cast<uint64_t*>(base + L.start), reinterpret_cast<uint64_t*>(base + L.cnt),
               reinterpret_cast<uint64_t*>(base + L.exit),  reinterpret_cast<uint32_t*>(base + L.stop),
               reinterpret_cast<uint32_t*>(base + L.bad),   reinterpret_cast<uint32_t*>(base + L.blk),
-              reinterpret_cast<uint32_t*>(base + L.ctl),   reinterpret_cast<uint64_t*>(base + L.list),
+              reinterpret_cast<uint32_t*>(base + L.ctl),   reinterpret_cast<uint8_t*>(base + L.list),
               static_cast<uint32_t>(L.cap)};
     auto* counts = reinterpret_cast<uint64_t*>(base + L.counts);
     auto* recbase = reinterpret_cast<uint64_t*>(base + L.recbase);
