@@ -138,6 +138,9 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
 #define SRPC_TUNE_NONTEMPORAL 3      /* bit0 non-temporal stores, bit1 loads      */
 #define SRPC_TUNE_TILE_BYTES 4       /* TILE path: target LDS image bytes per tile
                                         (1024..49152), pack and unpack           */
+#define SRPC_TUNE_WAVE_PACK_BYTES 11   /* TILE path: pack with one wave per tile of about this
+                                         many image bytes (0 = workgroup tiles)        */
+#define SRPC_TUNE_WAVE_UNPACK_BYTES 12 /* TILE path: the same for unpack                */
 #define SRPC_TUNE_PACK_TILE_BYTES 9  /* TILE path: the same for the pack kernel only */
 #define SRPC_TUNE_VAR_KERNEL 7       /* VAR: 1 = record tiles, one pass (default; unpack of
                                         records under 40 bytes on average keeps 0), 0 =

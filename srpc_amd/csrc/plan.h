@@ -183,7 +183,13 @@ struct srpc_plan {
     uint32_t ptile_R = 0;            // pack image kernel: records per tile
     size_t ptile_lds = 0;
     size_t tile_lds = 0;
-    bool all4 = false;               // every field 4 bytes (DWORD x4 variant eligible)
+    // TILE wave tiles (one wave per tile), per direction; R = 0: workgroup tiles
+    struct WaveTile {
+        uint32_t R = 0;              // records per tile
+        size_t lds = 0;
+        int k = 0, kw = 0;           // column chunks / wire chunks per lane
+    } wtp, wtu;                      // pack, unpack
+    bool all4 = false;              // every field 4 bytes (DWORD x4 variant eligible)
     srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
     // string schemas (SRPC_PATH_VAR)
     uint32_t nstrings = 0;

@@ -462,6 +462,203 @@ __global__ __launch_bounds__(kBlock) SRPC_FLAT_ATTR void k_pack_tile_flat(TileAr
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wave tiles: one wave owns a tile of R records (a workgroup of one wave), so
+// no phase waits on other waves -- the image needs only the wave's own LDS
+// ordering (s_waitcnt lgkmcnt(0)), never an s_barrier.  A workgroup tile's
+// stores cannot start until its slowest wave's loads are back; here every
+// wave streams load -> scatter -> store on its own, and the small image
+// (~4 KiB) lets 8 waves per SIMD stay resident.
+// ---------------------------------------------------------------------------
+constexpr int kWave = 64;
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void wave_template(const TileArgs& a, uint8_t* tmpl) {
+    const uint32_t nch = (2 * a.L) >> 4;
+    for (uint32_t i = threadIdx.x; i < nch; i += kWave)
+        reinterpret_cast<uint4*>(tmpl)[i] = reinterpret_cast<const uint4*>(a.period)[i];
+}
+
+// Item g of a tile -> (column pointer, element bytes, record offset, chunk):
+// every field's 16-byte column chunks numbered as one list, K items per lane
+// (g = lane + 64u).  Field values come from uniform (scalar) reads of the
+// kernarg arrays inside the uniform field loop.
+template <int K>
+struct WaveItems {
+    const uint8_t* col[K];
+    uint32_t sz[K], off[K], c[K];
+    uint32_t total;
+};
+
+template <int K>
+__device__ __forceinline__ void wave_items(const TileArgs& a, uint64_t rbase, uint32_t nr, WaveItems<K>& w) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t total = 0;
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        w.col[u] = nullptr;
+        w.sz[u] = w.off[u] = w.c[u] = 0;
+    }
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t s = a.size[f];
+        const uint8_t* base = a.col[f] + rbase * s;
+        const uint32_t off = a.off[f];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t g = lane + u * kWave;
+            if (g >= total) {
+                w.col[u] = base;
+                w.sz[u] = s;
+                w.off[u] = off;
+                w.c[u] = g - total;
+            }
+        }
+        total += (nr * s + 15) >> 4;
+    }
+    w.total = total;
+}
+
+template <int K>
+__global__ __launch_bounds__(kWave) void k_pack_tile_wave(TileArgs a, uint8_t* __restrict__ wire, uint64_t n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t T = a.R * a.stride;
+    uint8_t* img = lds;
+    uint8_t* tmpl = lds + T;
+    uint8_t* mask = tmpl + a.L;
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    WaveItems<K> w;
+    wave_items<K>(a, rbase, nr, w);
+    uint4 qq[K];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const uint32_t g = lane + u * kWave;
+        if (g < w.total && (w.c[u] + 1) * 16 <= nr * w.sz[u])
+            qq[u] = reinterpret_cast<const uint4*>(w.col[u])[w.c[u]];
+    }
+    if (a.prefix_len) wave_template(a, tmpl);
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const uint32_t g = lane + u * kWave;
+        if (g >= w.total) break;
+        const uint32_t s = w.sz[u], off = w.off[u], c = w.c[u];
+        const uint32_t lg = s == 1 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3;
+        const uint32_t e0 = (16 * c) >> lg;
+        const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+        if ((c + 1) * 16 > nr * s) {  // the column's last, partial chunk: whole elements, bytewise
+            for (uint32_t e = e0; e < nr; ++e)
+                for (uint32_t i = 0; i < s; ++i) img[e * a.stride + off + i] = w.col[u][e * s + i];
+            continue;
+        }
+        switch (s) {
+        case 1: scatter_chunk<1>(img, qq[u], e0, ne, a.stride, off); break;
+        case 2: scatter_chunk<2>(img, qq[u], e0, ne, a.stride, off); break;
+        case 4: scatter_chunk<4>(img, qq[u], e0, ne, a.stride, off); break;
+        default: scatter_chunk<8>(img, qq[u], e0, ne, a.stride, off); break;
+        }
+    }
+    wave_lds_sync();
+    uint8_t* dst = wire + rbase * a.stride;
+    const uint32_t tbytes = nr * a.stride;
+    const uint32_t full = tbytes >> 4;
+    for (uint32_t c = lane; c < full; c += kWave) {
+        uint4 v = *reinterpret_cast<const uint4*>(img + 16 * c);
+        if (a.prefix_len) {
+            const uint32_t ph = (16 * c) % a.L;
+            v = and_not_or(v, *reinterpret_cast<const uint4*>(mask + ph), *reinterpret_cast<const uint4*>(tmpl + ph));
+        }
+        __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + 16 * c));
+    }
+    if (lane == 0) {
+        for (uint32_t i = full * 16; i < tbytes; ++i) {
+            const uint32_t ph = i % a.L;
+            dst[i] = a.prefix_len && mask[ph] ? tmpl[ph] : img[i];
+        }
+    }
+}
+
+// Unpack of a wave tile: wire chunks (KW per lane, every prefix byte checked)
+// -> LDS image -> every field's column chunks as one list (K per lane).
+template <int K, int KW>
+__global__ __launch_bounds__(kWave) void k_unpack_tile_wave(TileArgs a, const uint8_t* __restrict__ wire, uint64_t n,
+                                                            srpc_unpack_status* st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t T = a.R * a.stride;
+    uint8_t* img = lds;
+    uint8_t* tmpl = lds + T;
+    uint8_t* mask = tmpl + a.L;
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    const uint8_t* src = wire + rbase * a.stride;
+    const uint32_t tbytes = nr * a.stride;
+    const uint32_t full = tbytes >> 4;
+    uint4 vv[KW];
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+        const uint32_t c = lane + u * kWave;
+        if (c < full) vv[u] = reinterpret_cast<const uint4*>(src)[c];
+    }
+    if (a.prefix_len) wave_template(a, tmpl);
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+        const uint32_t c = lane + u * kWave;
+        if (c >= full) break;
+        const uint4 v = vv[u];
+        if (a.prefix_len && st) {
+            const uint32_t ph = (16 * c) % a.L;
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + ph);
+            const uint4 t = *reinterpret_cast<const uint4*>(tmpl + ph);
+            const uint32_t d0 = (v.x & m.x) ^ t.x, d1 = (v.y & m.y) ^ t.y;
+            const uint32_t d2 = (v.z & m.z) ^ t.z, d3 = (v.w & m.w) ^ t.w;
+            if (d0 | d1 | d2 | d3) {
+                const uint32_t wd = d0 ? 0 : d1 ? 1 : d2 ? 2 : 3;
+                const uint32_t dw = d0 ? d0 : d1 ? d1 : d2 ? d2 : d3;
+                const uint32_t i = 16 * c + 4 * wd + (__builtin_ctz(dw) >> 3);
+                report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+            }
+        }
+        *reinterpret_cast<uint4*>(img + 16 * c) = v;
+    }
+    if (lane == 0) {
+        for (uint32_t i = full * 16; i < tbytes; ++i) {
+            const uint8_t b = src[i];
+            const uint32_t ph = i % a.L;
+            if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph]) report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+            img[i] = b;
+        }
+    }
+    wave_lds_sync();
+    WaveItems<K> w;
+    wave_items<K>(a, rbase, nr, w);
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const uint32_t g = lane + u * kWave;
+        if (g >= w.total) break;
+        const uint32_t s = w.sz[u], off = w.off[u], c = w.c[u];
+        const uint32_t lg = s == 1 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3;
+        const uint32_t e0 = (16 * c) >> lg;
+        const uint32_t ne = min<uint32_t>(16u >> lg, nr - e0);
+        uint8_t* dstc = const_cast<uint8_t*>(w.col[u]);
+        if ((c + 1) * 16 > nr * s) {  // the column's last, partial chunk: whole elements, bytewise
+            for (uint32_t e = e0; e < nr; ++e)
+                for (uint32_t i = 0; i < s; ++i) dstc[e * s + i] = img[e * a.stride + off + i];
+            continue;
+        }
+        uint4 q;
+        switch (s) {
+        case 1: q = gather_chunk<1>(img, e0, ne, a.stride, off); break;
+        case 2: q = gather_chunk<2>(img, e0, ne, a.stride, off); break;
+        case 4: q = gather_chunk<4>(img, e0, ne, a.stride, off); break;
+        default: q = gather_chunk<8>(img, e0, ne, a.stride, off); break;
+        }
+        __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w}, reinterpret_cast<u32x4*>(dstc) + c);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_t* __restrict__ wire,
                                                         uint64_t n, uint64_t ntiles,
                                                         srpc_unpack_status* st) {
@@ -797,6 +994,29 @@ void configure_pack_tile(srpc_plan* p, uint32_t target) {
     p->tile_flat_k = mixed && kTilePackFlat ? (k <= 1 ? 1 : k <= 2 ? 2 : k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 0) : 0;
 }
 
+inline int pow2_slots(uint32_t k) { return k <= 1 ? 1 : k <= 2 ? 2 : k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 0; }
+
+// Wave tiles of about `target` image bytes (0: workgroup tiles): R records, a
+// multiple of 16 (R*stride is then a multiple of 16), and the column and wire
+// chunk slots per lane.
+int configure_wave_tile(srpc_plan* p, srpc_plan::WaveTile& w, uint32_t target) {
+    w = srpc_plan::WaveTile{};
+    if (!target) return SRPC_OK;
+    const uint32_t S = static_cast<uint32_t>(p->stride);
+    const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
+    uint32_t allc = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) allc += (R * p->size[f] + 15) / 16;
+    const int k = pow2_slots((allc + kWave - 1) / kWave);
+    const int kw = pow2_slots((R * S / 16 + kWave - 1) / kWave);
+    const size_t lds = static_cast<size_t>(R) * S + (p->prefix_len ? 2 * p->tile_L : 0);
+    if (!k || !kw || lds > 65536) return SRPC_E_INVALID;
+    w.R = R;
+    w.lds = lds;
+    w.k = k;
+    w.kw = kw;
+    return SRPC_OK;
+}
+
 void configure_tile(srpc_plan* p, uint32_t target) {
     const uint32_t S = static_cast<uint32_t>(p->stride);
     const uint32_t R = 16 * std::max<uint32_t>(1, target / (16 * S));
@@ -933,6 +1153,14 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
         // through the caches) for the square request/response and Quad
         // (profiles/r01_ab_pack_tile.log, r01_sweep_tile.log)
         configure_pack_tile(p, p->prefix_len ? 24576 : 16384);
+        // records under 16 bytes without an envelope: wave tiles (pack 2 KiB,
+        // unpack 3 KiB images) -- 3-15-byte schemas 5-32 % faster both ways,
+        // 16-53-byte and enveloped ones as fast or slower, a lone int16 column
+        // unpacks faster with workgroup tiles (profiles/r02_wave_tile_sweep.log)
+        if (!p->prefix_len && o < 16) {
+            (void)configure_wave_tile(p, p->wtp, 2048);
+            if (o != 2) (void)configure_wave_tile(p, p->wtu, 3072);
+        }
         if (upload_period(p) != SRPC_OK) {
             (void)srpc_plan_destroy(p);
             return SRPC_E_HIP;
@@ -1018,6 +1246,12 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         p->rt_ch_cap = static_cast<uint32_t>(value);
         p->rt_ch_cap_auto = false;
         return SRPC_OK;
+    case SRPC_TUNE_WAVE_PACK_BYTES:
+        if (value < 0 || value > 65536 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
+        return configure_wave_tile(p, p->wtp, static_cast<uint32_t>(value));
+    case SRPC_TUNE_WAVE_UNPACK_BYTES:
+        if (value < 0 || value > 65536 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
+        return configure_wave_tile(p, p->wtu, static_cast<uint32_t>(value));
     case SRPC_TUNE_PACK_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_pack_tile(p, static_cast<uint32_t>(value));
@@ -1043,6 +1277,20 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
         DwordVariant v = p->dv;
         v.rpl = x4 ? 4 : 1;
         return launch_dword_any(true, m, wire, n, static_cast<uint32_t>(p->stride / 4), v, s);
+    }
+    if (p->wtp.R && n / p->wtp.R < (1ull << 26)) {
+        TileArgs a = make_tile_args(p, cols, true);
+        a.R = p->wtp.R;
+        const uint32_t grid = static_cast<uint32_t>((n + a.R - 1) / a.R);
+        const size_t lds = p->wtp.lds;
+        switch (p->wtp.k) {
+        case 1: launch(k_pack_tile_wave<1>, dim3(grid), dim3(kWave), lds, s, a, wire, n); break;
+        case 2: launch(k_pack_tile_wave<2>, dim3(grid), dim3(kWave), lds, s, a, wire, n); break;
+        case 4: launch(k_pack_tile_wave<4>, dim3(grid), dim3(kWave), lds, s, a, wire, n); break;
+        case 8: launch(k_pack_tile_wave<8>, dim3(grid), dim3(kWave), lds, s, a, wire, n); break;
+        default: launch(k_pack_tile_wave<16>, dim3(grid), dim3(kWave), lds, s, a, wire, n); break;
+        }
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     const TileArgs a = make_tile_args(p, cols, true);
     const uint64_t ptiles = (n + p->ptile_R - 1) / p->ptile_R;
@@ -1101,6 +1349,32 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         rc = launch_dword_any(false, m, const_cast<uint8_t*>(wire), n_fit,
                               static_cast<uint32_t>(p->stride / 4), v, s);
         return rc ? rc : ret;
+    }
+    if (p->wtu.R && n_fit / p->wtu.R < (1ull << 26)) {
+        TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
+        a.R = p->wtu.R;
+        const uint32_t grid = static_cast<uint32_t>((n_fit + a.R - 1) / a.R);
+        const size_t lds = p->wtu.lds;
+#define SRPC_UW(K, KW) launch(k_unpack_tile_wave<K, KW>, dim3(grid), dim3(kWave), lds, s, a, wire, n_fit, st)
+#define SRPC_UWK(K)                          \
+    switch (p->wtu.kw) {                   \
+    case 1: SRPC_UW(K, 1); break;            \
+    case 2: SRPC_UW(K, 2); break;            \
+    case 4: SRPC_UW(K, 4); break;            \
+    case 8: SRPC_UW(K, 8); break;            \
+    default: SRPC_UW(K, 16); break;          \
+    }
+        switch (p->wtu.k) {
+        case 1: SRPC_UWK(1); break;
+        case 2: SRPC_UWK(2); break;
+        case 4: SRPC_UWK(4); break;
+        case 8: SRPC_UWK(8); break;
+        default: SRPC_UWK(16); break;
+        }
+#undef SRPC_UWK
+#undef SRPC_UW
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+        return ret;
     }
     const uint64_t ntiles = (n_fit + p->tile_R - 1) / p->tile_R;
     const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);

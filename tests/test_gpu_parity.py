@@ -856,3 +856,58 @@ def test_multi_strings_errors(maxlen, vk):
     check(wire, rec4)
     # a truncated wire: the last records fall outside it
     check(bytes(wire[:int(rec[n - 5]) + 3]), rec)
+
+
+WAVE_SCHEMAS = {
+    "i8": ([oracle.INT8], b""),
+    "i16_i8": ([oracle.INT16, oracle.INT8], b""),
+    "bool_i32": ([oracle.BOOL, oracle.INT32], b""),
+    "i64_i32_i16_i8": ([oracle.INT64, oracle.INT32, oracle.INT16, oracle.INT8], b""),
+    "all_kinds": ([oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64], b""),
+    "i16_i64_prefix": ([oracle.INT16, oracle.INT64], b"abc"),
+    "quad": ([oracle.INT32] * 4, b""),
+}
+
+
+@pytest.mark.parametrize("wave", [0, 1024, 2048, 3072, 8192])
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 1023, 1025, 3001, 65_537])
+@pytest.mark.parametrize("schema", sorted(WAVE_SCHEMAS))
+def test_wave_tiles_vs_oracle(schema, n, wave):
+    """TILE kernels with one wave per tile (SRPC_TUNE_WAVE_PACK_BYTES /
+    WAVE_UNPACK_BYTES; 0 = workgroup tiles) at several tile sizes: partial
+    last tiles, partial column chunks, enveloped records, against the oracle."""
+    kinds, prefix = WAVE_SCHEMAS[schema]
+    rng = np.random.default_rng(n * 13 + len(kinds) + wave)
+    cols = []
+    for k in kinds:
+        c = rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(oracle.KIND_DTYPE[k])
+        cols.append((c & 1).astype(np.uint8) if k == oracle.BOOL else c)
+    p = GpuPacker(Schema("X", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    p.force_path(SRPC_PATH_TILE)
+    p.tune(wave_pack_bytes=wave, wave_unpack_bytes=wave)
+    want = oracle.pack(kinds, cols, n, prefix)
+    assert gpu_pack(p, cols, n) == want
+    rc, back = gpu_unpack(p, want, n, [oracle.KIND_DTYPE[k] for k in kinds])
+    assert rc == 0
+    for a, b in zip(cols, back):
+        assert a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("bad", [0, 63, 64, 1000])
+def test_wave_tile_prefix_mismatch_reported(bad):
+    """A corrupted envelope byte in a wave-tile unpack is reported at its
+    record, as the oracle's cursor reports it."""
+    kinds, prefix = WAVE_SCHEMAS["i16_i64_prefix"]
+    n = 2000
+    rng = np.random.default_rng(bad)
+    cols = [rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(oracle.KIND_DTYPE[k]) for k in kinds]
+    p = GpuPacker(Schema("X", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    p.tune(wave_unpack_bytes=2048)
+    wire = bytearray(oracle.pack(kinds, cols, n, prefix))
+    wire[bad * p.record_bytes + 1] ^= 0x40
+    st = status_buf()
+    rc, _ = gpu_unpack(p, bytes(wire), n, [oracle.KIND_DTYPE[k] for k in kinds], status=st)
+    flags, first = read_status(st)
+    assert flags == SRPC_STATUS_PREFIX and first == bad
+    st_o, _, _, _, err = oracle.unpack(kinds, bytes(wire), n, prefix)
+    assert st_o == oracle.ORC_ERR_PREFIX and err == bad
