@@ -33,15 +33,26 @@ __global__ __launch_bounds__(kBlock) void k_xscan_reduce(const T* __restrict__ v
     if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// One workgroup: exclusive scan of the nb block totals in place, thread t
-// owning a contiguous run of them; *total = their sum.
-__global__ __launch_bounds__(kBlock) void k_xscan_partials(uint64_t* __restrict__ part, uint64_t nb,
-                                                           uint64_t* __restrict__ total) {
-    __shared__ uint64_t ws[kBlock / 64];
-    const uint64_t per = (nb + kBlock - 1) / kBlock;
-    const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+// One workgroup of B threads: exclusive scan of the nb block totals in place,
+// thread t owning a contiguous run of them; *total = their sum.  Each run is
+// read and written 8 words per batch (independent loads in flight: a run of
+// 32 read word by word, one round trip each, took 17 us).
+template <int B>
+__global__ __launch_bounds__(B) void k_xscan_partials(uint64_t* __restrict__ part, uint64_t nb,
+                                                      uint64_t* __restrict__ total) {
+    __shared__ uint64_t ws[B / 64];
+    const uint64_t per = (nb + B - 1) / B;
+    const uint64_t lo = min<uint64_t>(threadIdx.x * per, nb), hi = min<uint64_t>(lo + per, nb);
     uint64_t s = 0;
-    for (uint64_t b = lo; b < hi; ++b) s += part[b];
+    uint64_t b = lo;
+    for (; b + 8 <= hi; b += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[b + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; b < hi; ++b) s += part[b];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t inc = s;
 #pragma unroll
@@ -53,12 +64,27 @@ __global__ __launch_bounds__(kBlock) void k_xscan_partials(uint64_t* __restrict_
     __syncthreads();
     uint64_t run = inc - s;
     for (int w = 0; w < wave; ++w) run += ws[w];
-    for (uint64_t b = lo; b < hi; ++b) {
+    b = lo;
+    for (; b + 8 <= hi; b += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[b + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            part[b + j] = run;
+            run += v[j];
+        }
+    }
+    for (; b < hi; ++b) {
         const uint64_t x = part[b];
         part[b] = run;
         run += x;
     }
-    if (threadIdx.x == kBlock - 1) *total = ws[0] + ws[1] + ws[2] + ws[3];
+    if (threadIdx.x == B - 1) {
+        uint64_t t = 0;
+        for (int w = 0; w < B / 64; ++w) t += ws[w];
+        *total = t;
+    }
 }
 
 template <typename T>
@@ -103,7 +129,7 @@ template <typename T>
 inline void xscan(const T* v, uint64_t n, uint64_t* part, uint64_t* total, uint64_t* out, hipStream_t s) {
     const uint64_t nb = (n + kXScanPer - 1) / kXScanPer;
     if (nb) launch(k_xscan_reduce<T>, dim3(static_cast<uint32_t>(nb)), dim3(kBlock), 0, s, v, n, part);
-    launch(k_xscan_partials, dim3(1), dim3(kBlock), 0, s, part, nb, total);
+    launch(k_xscan_partials<kBlock>, dim3(1), dim3(kBlock), 0, s, part, nb, total);
     launch(k_xscan_apply<T>, dim3(static_cast<uint32_t>(nb ? nb : 1)), dim3(kBlock), 0, s, v, n,
            static_cast<const uint64_t*>(part), static_cast<const uint64_t*>(total), out);
 }

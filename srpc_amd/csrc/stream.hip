@@ -455,10 +455,12 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
 __global__ __launch_bounds__(kBlock) void k_stream_check_edges(uint64_t W, uint64_t C, Chunks ch) {
     const uint64_t wg = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x + 1;  // workgroup 0 needs none
     if (wg * kBlock >= C) return;
+    // every chunk visited before the first with a record start passes the
+    // entry through: one look-back for the workgroup's leading chunks
+    bool stopped;
+    const uint64_t e = entry_of(ch, wg * kBlock, &stopped);
     for (uint64_t c = wg * kBlock; c < C && c < (wg + 1) * kBlock; ++c) {
         const uint64_t hi = min((c + 1) * kChunk, W);
-        bool stopped;
-        const uint64_t e = entry_of(ch, c, &stopped);
         const bool ok = stopped || agrees(e, hi, ch.start[c]);
         ch.bad[c] = ok ? 0u : 1u;
         if (!ok) {
@@ -471,18 +473,24 @@ __global__ __launch_bounds__(kBlock) void k_stream_check_edges(uint64_t W, uint6
 }
 
 // Parallel repair rounds (before the serial fixer): every bad chunk walks
-// again from its entry as it stands, then every chunk is checked again.  The
-// first bad chunk's entry is final, so each round repairs at least it, and
-// isolated mis-speculations (the common case: a start one byte early whose
-// u64 length reads as len * 256 + a char, ~1 % of chunks on random strings)
-// all in one round.  ctl[3] / ctl[4]: the recheck's any-bad / first-bad.
+// again from its entry as it stands, then the chunks whose entry may have
+// changed are checked again.  The first bad chunk's entry is final, so each
+// round repairs at least it, and isolated mis-speculations (the common case: a
+// start one byte early whose u64 length reads as len * 256 + a char) all in
+// one round.  Both kernels visit only 256-chunk blocks flagged in blk (bit 0:
+// holds a bad chunk; bit 2: follows a chunk walked again), a workgroup per
+// block on a grid-stride grid, so a round costs two launches of a few
+// thousand workgroups at most.  ctl[3] / ctl[4]: the recheck's any-bad / first-bad.
+constexpr uint32_t kBlkBad = 1, kBlkStop = 2, kBlkRecheck = 4;
+
 __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
                                                          uint64_t C, Chunks ch) {
     if (ch.ctl[0] == 0) return;
-    // grid-stride (a small grid: the launch is a no-op whenever every chunk agrees)
-    for (uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; c < C;
-         c += static_cast<uint64_t>(gridDim.x) * kBlock) {
-        if (!ch.bad[c]) continue;
+    const uint64_t nblk = (C + 255) / 256;
+    for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        if (!(ch.blk[b] & kBlkBad)) continue;  // uniform
+        const uint64_t c = b * 256 + threadIdx.x;
+        if (c >= C || !ch.bad[c]) continue;
         // only a chunk whose entry is final: no bad chunk between it and the chunk
         // that provides its entry (a chunk marked bad only because its
         // predecessor was wrong keeps its own, probably right, speculation)
@@ -509,15 +517,29 @@ __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uin
         ch.cnt[c] = cnt;
         ch.exit[c] = exit;
         ch.stop[c] = stop;
-        if (stop) atomicOr(&ch.blk[c >> 8], 2u);
+        if (stop) atomicOr(&ch.blk[c >> 8], kBlkStop);
+        // the chunks whose entry is this chunk's exit: up to and including the
+        // next one holding a record start
+        uint64_t mb = ~0ull;
+        for (uint64_t j = c + 1; j < C; ++j) {
+            if ((j >> 8) != mb) {
+                mb = j >> 8;
+                atomicOr(&ch.blk[mb], kBlkRecheck);
+            }
+            if (ch.start[j] != kNone) break;
+        }
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t C, Chunks ch) {
     if (ch.ctl[0] == 0) return;
-    // grid-stride, whole waves per step (note_bad ballots over the wave)
-    for (uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kBlock; c0 < C; c0 += static_cast<uint64_t>(gridDim.x) * kBlock) {
-        const uint64_t c = c0 + threadIdx.x;
+    const uint64_t nblk = (C + 255) / 256;
+    for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const uint32_t f = ch.blk[b];
+        if (!(f & (kBlkBad | kBlkRecheck))) continue;  // uniform: every chunk of the block agreed and kept its entry
+        __syncthreads();  // every lane has read blk[b] before it changes
+        if (threadIdx.x == 0 && (f & kBlkRecheck)) atomicAnd(&ch.blk[b], ~kBlkRecheck);
+        const uint64_t c = b * 256 + threadIdx.x;
         bool ok = true;
         if (c < C && c > 0) {
             const uint64_t hi = min((c + 1) * kChunk, W);
@@ -587,22 +609,54 @@ __global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_stream_mask(uint64_t C, Chunks ch, uint64_t* counts) {
-    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c < C) counts[c] = c > ch.ctl[1] ? 0 : ch.cnt[c];
+// Records of chunk c that enter the index: none past the stream's stop chunk.
+__device__ __forceinline__ uint64_t chunk_count(const Chunks& ch, uint64_t c, uint64_t C, uint64_t stopc) {
+    return c < C && c <= stopc ? ch.cnt[c] : 0;
 }
 
-// rec_offs[recbase[c] + k] = the chunk's k-th record start, up to index n
-// (a lane per chunk, from the starts its walk kept).
-__global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, const uint64_t* __restrict__ counts,
-                                                         const uint64_t* __restrict__ recbase, uint64_t n,
-                                                         uint64_t* __restrict__ rec_offs) {
+// Exclusive scan over the workgroup's 256 lanes; *total = their sum.
+__device__ __forceinline__ uint64_t wg_exclusive_scan(uint64_t x, uint64_t* total) {
+    __shared__ uint64_t ws[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint64_t before = inc - x;
+    for (int w = 0; w < wave; ++w) before += ws[w];
+    *total = ws[0] + ws[1] + ws[2] + ws[3];
+    return before;
+}
+
+// The index in three launches, with no per-chunk count or record-number
+// arrays: per 256 chunks the number of records (k_stream_count), the scan of
+// those block totals (k_xscan_partials), then per chunk its first record
+// number (a workgroup scan plus its block's total) and its starts
+// (k_stream_index) -- formerly a count array, a three-pass device scan into a
+// record-number array and the index pass (mask 10 + scan 33 + index 19 us on
+// 4M 0-64-byte strings).
+__global__ __launch_bounds__(kBlock) void k_stream_count(uint64_t C, Chunks ch, uint64_t* __restrict__ parts) {
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c >= C || counts[c] == 0) return;
-    const uint64_t r0 = recbase[c];
-    if (r0 > n) return;
+    uint64_t tot;
+    (void)wg_exclusive_scan(chunk_count(ch, c, C, ch.ctl[1]), &tot);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+// rec_offs[first record of chunk c + k] = the chunk's k-th record start, up
+// to index n (a lane per chunk, from the starts its walk kept).
+__global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, const uint64_t* __restrict__ parts,
+                                                         uint64_t n, uint64_t* __restrict__ rec_offs) {
+    const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t cnt = chunk_count(ch, c, C, ch.ctl[1]);
+    uint64_t tot;
+    const uint64_t r0 = parts[blockIdx.x] + wg_exclusive_scan(cnt, &tot);
+    if (cnt == 0 || r0 > n) return;
     const uint8_t* list = ch.list + c * ch.cap;
-    const uint64_t k1 = min<uint64_t>(counts[c], n - r0 + 1);  // [n]: the start of record n, if any
+    const uint64_t k1 = min<uint64_t>(cnt, n - r0 + 1);  // [n]: the start of record n, if any
     for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = c * kChunk + list[k];
 }
 
@@ -611,10 +665,10 @@ __global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, 
 // rec_offs[T + 1 .. n] = W.  With T >= n, rec_offs[n] = the start of record n
 // (or the end of record n - 1).
 __global__ __launch_bounds__(kBlock) void k_stream_tail(uint64_t W, uint64_t C, Chunks ch,
-                                                        const uint64_t* __restrict__ recbase, uint64_t n,
+                                                        const uint64_t* __restrict__ total, uint64_t n,
                                                         uint64_t* __restrict__ rec_offs) {
     const uint64_t S = ch.ctl[1];
-    const uint64_t T = recbase[C];  // total (the scan's last entry)
+    const uint64_t T = *total;
     const uint64_t end = (C && S < C && ch.start[S] != kNone) ? ch.exit[S] : W;
     const uint64_t gs = static_cast<uint64_t>(gridDim.x) * kBlock;
     for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; r <= n; r += gs) {
@@ -647,7 +701,7 @@ __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct StreamLayout {
-    uint64_t C, start, cnt, exit, counts, recbase, stop, bad, blk, ctl, parts, list, cap, total;
+    uint64_t C, start, cnt, exit, stop, bad, blk, ctl, parts, list, cap, total;
 };
 
 StreamLayout stream_layout(uint64_t wire_len, uint32_t fixed_bytes) {
@@ -660,10 +714,6 @@ StreamLayout stream_layout(uint64_t wire_len, uint32_t fixed_bytes) {
     o += r256(8 * L.C);
     L.exit = o;
     o += r256(8 * L.C);
-    L.counts = o;
-    o += r256(8 * L.C);
-    L.recbase = o;
-    o += r256(8 * (L.C + 1));
     L.stop = o;
     o += r256(4 * L.C);
     L.bad = o;
@@ -672,8 +722,8 @@ StreamLayout stream_layout(uint64_t wire_len, uint32_t fixed_bytes) {
     o += r256(4 * ((L.C + 255) / 256));
     L.ctl = o;
     o += 256;
-    L.parts = o;  // the chunk-count scan's block totals, then its total
-    o += r256(8 * (xscan_parts(L.C) + 1));
+    L.parts = o;  // records per 256 chunks (then their exclusive scan), then the total
+    o += r256(8 * ((L.C + kBlock - 1) / kBlock + 1));
     L.cap = 1 + kChunk / std::max<uint32_t>(fixed_bytes, 1);
     L.list = o;
     o += r256(L.C * L.cap);  // one byte per start
@@ -714,8 +764,6 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
               reinterpret_cast<uint32_t*>(base + L.bad),   reinterpret_cast<uint32_t*>(base + L.blk),
               reinterpret_cast<uint32_t*>(base + L.ctl),   reinterpret_cast<uint8_t*>(base + L.list),
               static_cast<uint32_t>(L.cap)};
-    auto* counts = reinterpret_cast<uint64_t*>(base + L.counts);
-    auto* recbase = reinterpret_cast<uint64_t*>(base + L.recbase);
     StreamArgs a{};
     for (uint32_t f = 0; f < p->nfields; ++f) a.size[f] = p->size[f];
     a.prefix = p->d_prefix;
@@ -730,13 +778,14 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     const TimedCall timed;
     const uint64_t nblk = (C + 255) / 256;
+    auto* parts = reinterpret_cast<uint64_t*>(base + L.parts);
     launch(k_stream_ctl_reset, dim3(static_cast<uint32_t>(std::min<uint64_t>((nblk + 255) / 256 + 1, 1024))),
            dim3(256), 0, s, ch, nblk);
     if (wire_len) {
         launch(k_stream_chunks, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
         const uint64_t ge = (g + kBlock - 1) / kBlock;  // a lane per workgroup of k_stream_chunks
         launch(k_stream_check_edges, dim3(static_cast<uint32_t>(ge)), dim3(kBlock), 0, s, wire_len, C, ch);
-        const uint32_t gr = static_cast<uint32_t>(std::min<uint64_t>(g, 2048));
+        const uint32_t gr = static_cast<uint32_t>(std::min<uint64_t>(nblk, 2048));
         for (int r = 0; r < kRepairRounds; ++r) {  // gated: no-ops once every chunk agrees
             launch(k_stream_refix, dim3(gr), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
             launch(k_stream_recheck, dim3(gr), dim3(kBlock), 0, s, wire_len, C, ch);
@@ -744,17 +793,15 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
         }
         launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
         launch(k_stream_fix, dim3(1), dim3(64), 0, s, a, wire, wire_len, C, ch);
-        launch(k_stream_mask, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch, counts);
-    } else {
-        launch(k_stream_mask, dim3(1), dim3(kBlock), 0, s, 0ull, ch, counts);
+        launch(k_stream_count, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch, parts);
     }
-    auto* parts = reinterpret_cast<uint64_t*>(base + L.parts);
-    xscan(static_cast<const uint64_t*>(counts), wire_len ? C : 0ull, parts, parts + xscan_parts(C), recbase, s);
+    const uint64_t nb = wire_len ? g : 0;
+    launch(k_xscan_partials<1024>, dim3(1), dim3(1024), 0, s, parts, nb, parts + g);
     if (wire_len)
         launch(k_stream_index, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch,
-               static_cast<const uint64_t*>(counts), static_cast<const uint64_t*>(recbase), n, rec_offs);
+               static_cast<const uint64_t*>(parts), n, rec_offs);
     launch(k_stream_tail, dim3(static_cast<uint32_t>(std::min<uint64_t>(n / kBlock + 1, 4096))), dim3(kBlock), 0, s,
-           wire_len, wire_len ? C : 0ull, ch, static_cast<const uint64_t*>(recbase), n, rec_offs);
+           wire_len, wire_len ? C : 0ull, ch, static_cast<const uint64_t*>(parts + g), n, rec_offs);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     // the indexed decode over the index just built (the timing hook, if armed,
     // covers the index kernels above only)

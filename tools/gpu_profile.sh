@@ -5,7 +5,8 @@ set -o pipefail
 R=${1:-r01}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-BENCH="python3 bench.py --cpu-seconds 0 --no-pcie --no-verify"
+# the strong-scaling line (64M records) is left out so every launch is a 16M one
+BENCH="python3 bench.py --cpu-seconds 0 --no-pcie --no-verify --strong-records 0"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_${R}.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- $BENCH --steps 20 --warmup 3 > gpurun_out/prof_stats.log 2>&1 || exit 3
