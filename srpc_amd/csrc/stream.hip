@@ -44,10 +44,15 @@
 #include "scan.h"
 #include "srpc_gpu.h"
 
+
 namespace srpc_impl {
 namespace {
 
-constexpr uint32_t kChunk = 64;     // wire bytes per speculating lane
+#ifndef SRPC_STREAM_CHUNK
+#define SRPC_STREAM_CHUNK 64
+#endif
+constexpr uint32_t kChunk = SRPC_STREAM_CHUNK;  // wire bytes per speculating lane (<= 64: the filter's mask)
+static_assert(kChunk <= 64 && kChunk % 16 == 0, "a chunk's positions fit one 64-bit mask; 16-byte window reads");
 // records that must parse from a candidate start: with an envelope prefix of
 // 8 bytes or more a wrong start essentially never matches it, so one; else 2
 // (a wrong start that hops onto a true one passes any count: see k_stream_scan)
@@ -281,6 +286,47 @@ __device__ __forceinline__ void note_bad(const Chunks& ch, uint64_t c, bool bad,
     }
 }
 
+// The N dwords at LDS byte offset o & ~3 of the stage, in 16-byte reads (o
+// mod 16 is the same for every lane of the workgroup: chunks are a multiple
+// of 16 bytes apart, so the dword shift is a uniform switch).  Lanes' windows
+// sit kChunk bytes apart on the same banks: dword reads made the 19-dword
+// window 19 conflicted LDS ops (82 % of LDS cycles conflicted); 6 wide reads
+// cut the stream decode 7-12 % (profiles/r02_stream_window_ab.log).
+template <int N>
+__device__ __forceinline__ void lds_window(const uint8_t* st, uint32_t o, uint32_t (&d)[N]) {
+    constexpr int NQ = (N + 3 + 3) / 4;
+    uint32_t w[4 * NQ];
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    typedef const u32x4v __attribute__((address_space(3))) lds_u32x4c;
+    lds_u32x4c* q = reinterpret_cast<lds_u32x4c*>((lds_u8c*)st + (o & ~15u));
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const u32x4v v = q[i];
+        w[4 * i] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+    switch (__builtin_amdgcn_readfirstlane((o >> 2) & 3)) {
+    case 0:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k];
+        break;
+    case 1:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 1];
+        break;
+    case 2:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 2];
+        break;
+    default:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 3];
+        break;
+    }
+}
+
 // Chunk c's speculation and walk (k_stream_chunks, a lane per chunk of
 // kChunk bytes): a workgroup stages its kBlock chunks plus a margin in LDS
 // (LDS-DMA), and every lane, from LDS, finds its chunk's first plausible
@@ -346,9 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
         {
             uint32_t d[kChunk / 4 + 3];
             const uint32_t o = at + a.first_len_at, sh = o & 3;
-            lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)st + (o & ~3u));
-#pragma unroll
-            for (int k = 0; k < kChunk / 4 + 3; ++k) d[k] = q[k];
+            lds_window(st, o, d);
 #pragma unroll
             for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
             // position j: bytes j .. j + 7 of the shifted window
@@ -371,9 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
         if (a.prefix_len && mask) {
             uint32_t d[kChunk / 4 + 3];
             const uint32_t sh = at & 3;
-            lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)st + (at & ~3u));
-#pragma unroll
-            for (int k = 0; k < kChunk / 4 + 3; ++k) d[k] = q[k];
+            lds_window(st, at, d);
 #pragma unroll
             for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
             const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
@@ -480,12 +522,27 @@ __global__ __launch_bounds__(kBlock) void k_stream_check_edges(uint64_t W, uint6
 // one round.  Both kernels visit only 256-chunk blocks flagged in blk (bit 0:
 // holds a bad chunk; bit 2: follows a chunk walked again), a workgroup per
 // block on a grid-stride grid, so a round costs two launches of a few
-// thousand workgroups at most.  ctl[3] / ctl[4]: the recheck's any-bad / first-bad.
+// thousand workgroups at most.
 constexpr uint32_t kBlkBad = 1, kBlkStop = 2, kBlkRecheck = 4;
+// Round r's recheck writes its any-bad / first-bad to ctl[kCtlRound + 2r] /
+// [+ 1]; round r runs when the state before it (round r - 1's, or the first
+// check's ctl[0] / ctl[2]) has a bad chunk -- no launch between rounds.
+constexpr uint32_t kCtlRound = 8;
+__device__ __forceinline__ uint32_t round_in(uint32_t r) { return r ? kCtlRound + 2 * (r - 1) : 0; }
+// The state after the last round that ran: any bad chunk, *first = the first.
+__device__ __forceinline__ bool final_bad(const Chunks& ch, uint32_t* first) {
+    uint32_t any = ch.ctl[0];
+    *first = ch.ctl[2];
+    for (uint32_t r = 0; r < kRepairRounds && any; ++r) {
+        any = ch.ctl[kCtlRound + 2 * r];
+        *first = ch.ctl[kCtlRound + 2 * r + 1];
+    }
+    return any != 0;
+}
 
 __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
-                                                         uint64_t C, Chunks ch) {
-    if (ch.ctl[0] == 0) return;
+                                                         uint64_t C, Chunks ch, uint32_t round) {
+    if (ch.ctl[round_in(round)] == 0) return;
     const uint64_t nblk = (C + 255) / 256;
     for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
         if (!(ch.blk[b] & kBlkBad)) continue;  // uniform
@@ -531,8 +588,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uin
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t C, Chunks ch) {
-    if (ch.ctl[0] == 0) return;
+__global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t C, Chunks ch, uint32_t round) {
+    if (ch.ctl[round_in(round)] == 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ch.ctl[5], 1u);  // rounds that found something to repair
     const uint64_t nblk = (C + 255) / 256;
     for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
         const uint32_t f = ch.blk[b];
@@ -548,23 +606,17 @@ __global__ __launch_bounds__(kBlock) void k_stream_recheck(uint64_t W, uint64_t 
             ok = stopped || agrees(e, hi, ch.start[c]);
             ch.bad[c] = ok ? 0u : 1u;
         }
-        note_bad(ch, c, !ok, 3, 4);
+        note_bad(ch, c, !ok, kCtlRound + 2 * round, kCtlRound + 2 * round + 1);
     }
 }
 
-__global__ void k_stream_round_end(Chunks ch) {
-    if (threadIdx.x != 0 || ch.ctl[0] == 0) return;
-    ch.ctl[0] = ch.ctl[3];
-    ch.ctl[2] = ch.ctl[4];
-    ch.ctl[3] = 0;
-    ch.ctl[4] = 0xffffffffu;
-    ch.ctl[5] += 1;  // rounds that found something to repair (diagnostic)
-}
 
 // The stream's stop among the chunks before the first bad one (all right).// The stream's stop among the chunks before the first bad one (all right).
 __global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (c < C && c < ch.ctl[2] && ch.stop[c] && ch.start[c] != kNone)
+    uint32_t first;
+    (void)final_bad(ch, &first);
+    if (c < C && c < first && ch.stop[c] && ch.start[c] != kNone)
         atomicMin(&ch.ctl[1], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
 }
 
@@ -573,9 +625,11 @@ __global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
 // predecessor's (corrected) exit until the stream stops.  Chunks that agree
 // are kept; 256-chunk blocks with no bad chunk and no stop are skipped.
 __global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W, uint64_t C, Chunks ch) {
-    if (threadIdx.x != 0 || ch.ctl[0] == 0 || ch.ctl[1] < ch.ctl[2]) return;
+    if (threadIdx.x != 0) return;
+    uint32_t first;
+    if (!final_bad(ch, &first) || ch.ctl[1] < first) return;
     ch.ctl[6] = 1;
-    uint64_t c = ch.ctl[2];
+    uint64_t c = first;
     while (c < C) {
         const uint64_t hi = min((c + 1) * kChunk, W);
         bool stopped;
@@ -688,10 +742,12 @@ __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
         ch.ctl[0] = 0;            // some chunk is bad
         ch.ctl[1] = 0xffffffffu;  // the chunk where the stream stops
         ch.ctl[2] = 0xffffffffu;  // the first bad chunk
-        ch.ctl[3] = 0;            // repair round: any bad
-        ch.ctl[4] = 0xffffffffu;  // repair round: first bad
         ch.ctl[5] = 0;            // repair rounds run
         ch.ctl[6] = 0;            // the serial fixer ran
+        for (uint32_t r = 0; r < kRepairRounds; ++r) {
+            ch.ctl[kCtlRound + 2 * r] = 0;                // round r: any bad
+            ch.ctl[kCtlRound + 2 * r + 1] = 0xffffffffu;  // round r: first bad
+        }
     }
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nblk;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
@@ -787,9 +843,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
         launch(k_stream_check_edges, dim3(static_cast<uint32_t>(ge)), dim3(kBlock), 0, s, wire_len, C, ch);
         const uint32_t gr = static_cast<uint32_t>(std::min<uint64_t>(nblk, 2048));
         for (int r = 0; r < kRepairRounds; ++r) {  // gated: no-ops once every chunk agrees
-            launch(k_stream_refix, dim3(gr), dim3(kBlock), 0, s, a, wire, wire_len, C, ch);
-            launch(k_stream_recheck, dim3(gr), dim3(kBlock), 0, s, wire_len, C, ch);
-            launch(k_stream_round_end, dim3(1), dim3(64), 0, s, ch);
+            launch(k_stream_refix, dim3(gr), dim3(kBlock), 0, s, a, wire, wire_len, C, ch, static_cast<uint32_t>(r));
+            launch(k_stream_recheck, dim3(gr), dim3(kBlock), 0, s, wire_len, C, ch, static_cast<uint32_t>(r));
         }
         launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
         launch(k_stream_fix, dim3(1), dim3(64), 0, s, a, wire, wire_len, C, ch);
