@@ -735,6 +735,9 @@ constexpr uint64_t kWalkStageMax = 49152;
 #ifndef SRPC_STAGE_NUM
 #define SRPC_STAGE_NUM 17
 #endif
+#ifndef SRPC_RTU_OFFLOAD
+#define SRPC_RTU_OFFLOAD 1  // look-back waves' records built by the other waves (two strings 279 -> 270 us)
+#endif
 #ifndef SRPC_STAGE_DEN
 #define SRPC_STAGE_DEN 16
 #endif
@@ -1823,8 +1826,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     __shared__ uint64_t s_tot[kMaxFields], s_pre[kMaxFields];
     __shared__ uint32_t s_ioff[kMaxFields];
     __shared__ uint32_t s_ngran, s_fits;
+#if SRPC_RTU_OFFLOAD
+    __shared__ uint32_t s_bnd[kBlock / 32];  // records whose strings are not copied (BOUNDS, or past the tile)
+#endif
     const uint32_t lane = threadIdx.x & 63, i = threadIdx.x;
     const uint32_t ns = a.nstrings;
+#if SRPC_RTU_OFFLOAD
+    if (i < kBlock / 32) s_bnd[i] = 0;
+#endif
 #if SRPC_RTU_TICKET
     if (i == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
@@ -1903,6 +1912,9 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     } else {
         for (uint32_t k = 0; k < ns; ++k) len_l[k * kBlock + i] = 0;
     }
+#if SRPC_RTU_OFFLOAD
+    if (flag == SRPC_STATUS_BOUNDS) atomicOr(&s_bnd[i >> 5], 1u << (i & 31));
+#endif
     __syncthreads();
     PHASE(2);
     // per string field: offsets inside the tile, tile totals
@@ -1949,8 +1961,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     auto rd = [&](uint64_t p) -> uint64_t {
         return in_stage ? lds_u64(lds, sb + static_cast<uint32_t>(p - sw)) : load_unaligned<uint64_t>(wire + p);
     };
-    auto build = [&]() {
-        if (!fits || flag == SRPC_STATUS_BOUNDS) return;
+    // record j's chars into the image (its wire start, whether it is staged)
+    auto build_at = [&](uint32_t j, uint64_t start, bool in_stage) {
         uint64_t pos = start + a.prefix_len;
         uint32_t k = 0;
         for (uint32_t f = 0; f < a.nfields; ++f) {
@@ -1960,8 +1972,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
                 continue;
             }
             pos += 8;  // the length (the scan's offsets give it back)
-            const uint64_t o = len_l[k * kBlock + i];
-            const uint64_t len = (i + 1 < kBlock ? len_l[k * kBlock + i + 1] : s_tot[k]) - o;
+            const uint64_t o = len_l[k * kBlock + j];
+            const uint64_t len = (j + 1 < kBlock ? len_l[k * kBlock + j + 1] : s_tot[k]) - o;
             if (len) {
                 const uint32_t d = L.img_at + s_ioff[k] + static_cast<uint32_t>(o);
                 if (in_stage) {
@@ -1979,6 +1991,9 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
             ++k;
         }
     };
+    auto build = [&]() {
+        if (fits && flag != SRPC_STATUS_BOUNDS) build_at(i, start, in_stage);
+    };
     // string field si's look-back runs on wave si mod 4: the fields' round
     // trips overlap instead of adding up (two strings: one wave each)
     if (!kOpt && (i >> 6) < ns) {
@@ -1993,7 +2008,24 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         }
         if (stalled && lane == 0 && st) report_bad(st, SRPC_STATUS_STALLED, r0);
     }
+#if SRPC_RTU_OFFLOAD
+    // the waves that do not look back build every record's chars (the
+    // look-back waves' records too), so the look-back is off the build's path
+    if (!kOpt && ns < kBlock / 64) {
+        const uint32_t w = i >> 6, nb = kBlock - 64 * ns;
+        if (w >= ns && fits) {
+            for (uint32_t j = i - 64 * ns; j < nr; j += nb) {
+                if ((s_bnd[j >> 5] >> (j & 31)) & 1) continue;
+                const uint64_t sj = rec_offs[r0 + j], ej = rec_offs[r0 + j + 1];
+                build_at(j, sj, staged && sj >= slo && ej <= shi && sj <= ej);
+            }
+        }
+    } else {
+        build();
+    }
+#else
     build();
+#endif
     __syncthreads();
     PHASE(4);
     // 4. str_offs and chars, per string field; chunk c of the output covers
