@@ -524,6 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_check_edges(uint64_t W, uint6
 // block on a grid-stride grid, so a round costs two launches of a few
 // thousand workgroups at most.
 constexpr uint32_t kBlkBad = 1, kBlkStop = 2, kBlkRecheck = 4;
+constexpr uint32_t kChainMax = 64;  // chunks one repair lane walks behind its own
 // Round r's recheck writes its any-bad / first-bad to ctl[kCtlRound + 2r] /
 // [+ 1]; round r runs when the state before it (round r - 1's, or the first
 // check's ctl[0] / ctl[2]) has a bad chunk -- no launch between rounds.
@@ -575,10 +576,39 @@ __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uin
         ch.exit[c] = exit;
         ch.stop[c] = stop;
         if (stop) atomicOr(&ch.blk[c >> 8], kBlkStop);
-        // the chunks whose entry is this chunk's exit: up to and including the
-        // next one holding a record start
+        // the chain behind it: the following chunks that no longer agree with
+        // their (new) entry are walked again here, in order, up to the first
+        // that agrees -- runs of mis-speculated chunks (short records) are
+        // repaired in one round instead of one chunk per round.  Every chunk
+        // written and the chunks up to the next record start are rechecked.
+        uint64_t ent = start != kNone ? exit : e;
+        bool stp = start != kNone && stop != 0;
         uint64_t mb = ~0ull;
-        for (uint64_t j = c + 1; j < C; ++j) {
+        uint64_t j = c + 1;
+        for (uint32_t steps = 0; j < C && steps < kChainMax && !stp; ++j, ++steps) {
+            if ((j >> 8) != mb) {
+                mb = j >> 8;
+                atomicOr(&ch.blk[mb], kBlkRecheck);
+            }
+            const uint64_t hj = min((j + 1) * kChunk, W);
+            if (agrees(ent, hj, ch.start[j])) break;
+            uint64_t cnt2 = 0, exit2 = kNone, start2 = kNone;
+            uint32_t stop2 = 0;
+            if (ent < hj) {
+                start2 = ent;
+                walk(a, w, W, ent, hj, &cnt2, &exit2, &stop2, ch.list + j * ch.cap, ch.cap);
+            }
+            ch.start[j] = start2;
+            ch.cnt[j] = cnt2;
+            ch.exit[j] = exit2;
+            ch.stop[j] = stop2;
+            if (stop2) atomicOr(&ch.blk[j >> 8], kBlkStop);
+            if (start2 != kNone) {
+                ent = exit2;
+                stp = stop2 != 0;
+            }
+        }
+        for (; j < C; ++j) {  // up to and including the next chunk with a record start
             if ((j >> 8) != mb) {
                 mb = j >> 8;
                 atomicOr(&ch.blk[mb], kBlkRecheck);
