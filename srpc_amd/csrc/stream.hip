@@ -732,16 +732,31 @@ __global__ __launch_bounds__(kBlock) void k_stream_count(uint64_t C, Chunks ch, 
 
 // rec_offs[first record of chunk c + k] = the chunk's k-th record start, up
 // to index n (a lane per chunk, from the starts its walk kept).
+// The workgroup's starts go through LDS when they fit (kIndexStage entries):
+// a lane per chunk writes its few starts at scattered 8-byte slots, the
+// staged copy leaves as contiguous 512-byte wave stores.
+constexpr uint32_t kIndexStage = 2048;
 __global__ __launch_bounds__(kBlock) void k_stream_index(uint64_t C, Chunks ch, const uint64_t* __restrict__ parts,
                                                          uint64_t n, uint64_t* __restrict__ rec_offs) {
+    __shared__ uint64_t stage[kIndexStage];
     const uint64_t c = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const uint64_t cnt = chunk_count(ch, c, C, ch.ctl[1]);
     uint64_t tot;
-    const uint64_t r0 = parts[blockIdx.x] + wg_exclusive_scan(cnt, &tot);
-    if (cnt == 0 || r0 > n) return;
+    const uint64_t loc = wg_exclusive_scan(cnt, &tot);
+    const uint64_t base = parts[blockIdx.x];
+    if (base > n) return;  // uniform: every record of this workgroup is past n
+    const uint64_t r0 = base + loc;
     const uint8_t* list = ch.list + c * ch.cap;
-    const uint64_t k1 = min<uint64_t>(cnt, n - r0 + 1);  // [n]: the start of record n, if any
-    for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = c * kChunk + list[k];
+    if (tot > kIndexStage) {  // uniform
+        if (cnt == 0 || r0 > n) return;
+        const uint64_t k1 = min<uint64_t>(cnt, n - r0 + 1);  // [n]: the start of record n, if any
+        for (uint64_t k = 0; k < k1; ++k) rec_offs[r0 + k] = c * kChunk + list[k];
+        return;
+    }
+    for (uint64_t k = 0; k < cnt; ++k) stage[loc + k] = c * kChunk + list[k];
+    __syncthreads();
+    const uint64_t m = min<uint64_t>(tot, n - base + 1);  // entries up to index n
+    for (uint32_t i = threadIdx.x; i < m; i += kBlock) rec_offs[base + i] = stage[i];
 }
 
 // Records the stream holds: T = sum of counts.  rec_offs[T] = where the stream
