@@ -312,7 +312,18 @@ def main() -> None:
     t_rank = max(elapsed, gpu_ms / 1e3)
     t = torch.tensor([t_rank, sum(pack_ms) / K, sum(unpack_ms) / K], dtype=torch.float64,
                      device=dev if args.dist_backend == "nccl" else "cpu")
+    # per-rank view before the max: each rank's own kernel clock and what its
+    # RCCL communicator says it is (srpc_comm_rank), so a multi-GPU line shows
+    # that RCCL saw every rank
+    mine = {"rank": rank, "device": local, "pack_ms": round(sum(pack_ms) / K, 4),
+            "unpack_ms": round(sum(unpack_ms) / K, 4),
+            "frac": round(ALG_BYTES_PER_REC * n / (max(sum(pack_ms), sum(unpack_ms)) / K / 1e3) / 1e9
+                          / HBM_PEAK_GBPS, 4),
+            "rccl": comm.info() if comm is not None else None}
+    per_rank = [mine]
     if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max, pack_avg, unpack_avg = t.tolist()
     ms_step = t_max * 1e3 / K
@@ -420,6 +431,11 @@ def main() -> None:
         value = total_recs * K * REC_BYTES / 2**30 / t_max  # wire GiB/s, all ranks
         dom_name, dom_ms = ("pack", pack_avg) if pack_avg >= unpack_avg else ("unpack", unpack_avg)
         achieved = ALG_BYTES_PER_REC * n / (dom_ms / 1e3) / 1e9
+        # the same kernel from a cold Infinity Cache (512 MiB written before each
+        # call): the warm figure above is partly served on-die, cold is not
+        frac_cold = None
+        if cold:
+            frac_cold = round(ALG_BYTES_PER_REC * n / (cold[dom_name] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
         traffic = rocprof_us = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
@@ -456,6 +472,10 @@ def main() -> None:
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "frac_of_measured_copy": round(achieved / HBM_MEASURED_COPY_GBPS, 4),
+                         "frac_cold": frac_cold,
+                         "regime": "frac: warm steps (back to back; the 256 MiB Infinity Cache holds part "
+                                   "of the previous call's output); frac_cold: the same kernel after a "
+                                   "512 MiB flush",
                          "alg_bytes_per_launch": ALG_BYTES_PER_REC * n,
                          "traffic": traffic,
                          "committed_rocprof_avg_us": rocprof_us},
@@ -463,6 +483,14 @@ def main() -> None:
         }
         if gather:
             line["gather"] = gather
+        if world > 1:
+            seen = [r["rccl"] for r in per_rank]
+            line["rccl"] = {"ranks_seen": [r["rank"] for r in seen] if all(seen) else None,
+                            "nranks_seen": sorted({r["nranks"] for r in seen}) if all(seen) else None,
+                            "collective": gather["collective"] if gather else None,
+                            "note": None if all(seen) else (comm_note or "no libsrpc_gpu communicator "
+                                                            f"(--dist-backend {args.dist_backend})")}
+        line["per_rank"] = per_rank
         if strong:
             with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
                 streams = json.load(f)["streams"]

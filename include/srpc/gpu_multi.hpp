@@ -15,6 +15,7 @@
 
 #include <array>
 #include <cstdint>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -83,15 +84,28 @@ public:
     }
     device_group(device_group const&) = delete;
     device_group& operator=(device_group const&) = delete;
-    ~device_group() {
-        for (srpc_comm* c : _c)
-            if (c) srpc_comm_destroy(c);
+    /// Moves hand the communicators over; the source keeps none to destroy.
+    device_group(device_group&& o) noexcept : _dev(std::move(o._dev)), _c(std::move(o._c)) { o._c.clear(); }
+    device_group& operator=(device_group&& o) noexcept {
+        if (this != &o) {
+            release();
+            _dev = std::move(o._dev);
+            _c = std::move(o._c);
+            o._c.clear();
+        }
+        return *this;
     }
+    ~device_group() { release(); }
     int size() const { return static_cast<int>(_dev.size()); }
     int device(int g) const { return _dev[static_cast<size_t>(g)]; }
     srpc_comm* const* comms() const { return _c.data(); }
 
 private:
+    void release() noexcept {
+        for (srpc_comm* c : _c)
+            if (c) srpc_comm_destroy(c);
+        _c.clear();
+    }
     std::vector<int> _dev;
     std::vector<srpc_comm*> _c;
 };

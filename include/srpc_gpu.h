@@ -276,7 +276,10 @@ int srpc_allgather_u64(srpc_comm* comm, const uint64_t* d_in, uint64_t* d_out, v
 /* Gather: every rank calls it with its shard's wire bytes; the root receives
  * shard r at byte offset sum(h_all_bytes[0..r)) of d_root_wire (root_cap
  * bytes) -- the single-GPU wire of the whole batch.  h_all_bytes (host, one
- * entry per rank) is needed on the root only.  Stream-ordered. */
+ * entry per rank) is needed on the root only.  Stream-ordered.  Every
+ * argument is checked before the RCCL group is opened; if an operation then
+ * cannot be enqueued the group is ended unlaunched and the communicators it
+ * touched are aborted (later calls on them return SRPC_E_INVALID). */
 int srpc_gather_wire(srpc_comm* comm, const uint8_t* d_shard, uint64_t shard_bytes,
                      uint8_t* d_root_wire, uint64_t root_cap, const uint64_t* h_all_bytes,
                      int root, void* stream);
@@ -301,7 +304,9 @@ int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comm
  * the last frame ending at buf_len) into bucket k when it is exactly one record
  * of req_plans[k] -- a fixed-size plan whose prefix is the frame's constant
  * `BE32 len | str(method) | str(Req::name)`: same length, same prefix; the
- * first matching plan wins.  Outputs (device):
+ * first matching plan wins.  A frame whose offsets are out of order or run
+ * past buf_len is SRPC_FRAME_UNKNOWN (no byte outside d_buf is read).
+ * Outputs (device):
  *   d_class[i]             k, or SRPC_FRAME_UNKNOWN (the caller answers it);
  *   d_index[k*nframes + j] the frames of bucket k (j < d_counts[k]; order
  *                          within a bucket is unspecified);

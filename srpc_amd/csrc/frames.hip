@@ -52,7 +52,10 @@ __global__ __launch_bounds__(kBlock) void k_classify(ClassArgs a, const uint8_t*
     if (i < nf) {
         const uint64_t o = offs[i];
         const uint64_t end = i + 1 < nf ? offs[i + 1] : buf_len;
-        for (uint32_t p = 0; p < a.nplans && k == kNoClass; ++p) {
+        // offsets out of order or past the buffer: the frame is no plan's (the
+        // caller answers it), and no byte outside [0, buf_len) is read
+        const bool inside = o <= end && end <= buf_len;
+        for (uint32_t p = 0; inside && p < a.nplans && k == kNoClass; ++p) {
             if (end - o != a.frame_bytes[p] || a.prefix_len[p] > end - o) continue;
             const uint8_t* f = buf + o;
             const uint8_t* q = a.prefix[p];

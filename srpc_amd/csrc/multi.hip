@@ -36,6 +36,24 @@ using namespace srpc_impl;
 
 int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? SRPC_OK : SRPC_E_HIP; }
 
+// Ends a group of sends / receives.  When an operation could not be enqueued
+// (rc != OK), the group is half built: RCCL's ncclGroupEnd returns the stored
+// error without launching it, and every communicator it touched is aborted
+// (ncclCommAbort), so no peer waits on a live communicator for an operation
+// that will never come; those comms then refuse further work (comm = NULL)
+// and srpc_comm_destroy only frees them.
+int close_group(int rc, srpc_comm* const* comms, int n) {
+    const int end = nccl_rc(ncclGroupEnd());
+    if (rc == SRPC_OK) return end;
+    for (int g = 0; g < n; ++g)
+        if (comms[g] && comms[g]->comm) {
+            DeviceGuard dg(comms[g]->device);
+            (void)ncclCommAbort(comms[g]->comm);
+            comms[g]->comm = nullptr;
+        }
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -122,14 +140,14 @@ int srpc_comm_rank(const srpc_comm* c, int* rank, int* nranks) {
 }
 
 int srpc_allgather_u64(srpc_comm* c, const uint64_t* d_in, uint64_t* d_out, void* stream) {
-    if (!c || !d_in || !d_out) return SRPC_E_INVALID;
+    if (!c || !c->comm || !d_in || !d_out) return SRPC_E_INVALID;
     DeviceGuard g(c->device);
     return nccl_rc(ncclAllGather(d_in, d_out, 1, ncclUint64, c->comm, static_cast<hipStream_t>(stream)));
 }
 
 int srpc_gather_wire(srpc_comm* c, const uint8_t* d_shard, uint64_t shard_bytes, uint8_t* d_root_wire,
                      uint64_t root_cap, const uint64_t* h_all_bytes, int root, void* stream) {
-    if (!c || root < 0 || root >= c->nranks) return SRPC_E_INVALID;
+    if (!c || !c->comm || root < 0 || root >= c->nranks) return SRPC_E_INVALID;
     if (shard_bytes && !d_shard) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     DeviceGuard g(c->device);
@@ -137,11 +155,16 @@ int srpc_gather_wire(srpc_comm* c, const uint8_t* d_shard, uint64_t shard_bytes,
         if (!shard_bytes) return SRPC_OK;
         return nccl_rc(ncclSend(d_shard, shard_bytes, ncclUint8, root, c->comm, s));
     }
-    if (!h_all_bytes || (!d_root_wire && root_cap)) return SRPC_E_INVALID;
+    // the root: every argument checked before the group is opened
+    if (!h_all_bytes) return SRPC_E_INVALID;
     uint64_t total = 0;
-    for (int r = 0; r < c->nranks; ++r) total += h_all_bytes[r];
+    for (int r = 0; r < c->nranks; ++r) {
+        if (h_all_bytes[r] > ~0ull - total) return SRPC_E_INVALID;
+        total += h_all_bytes[r];
+    }
     if (h_all_bytes[root] != shard_bytes) return SRPC_E_INVALID;
     if (total > root_cap) return SRPC_E_CAPACITY;
+    if (total && !d_root_wire) return SRPC_E_INVALID;
     if (ncclGroupStart() != ncclSuccess) return SRPC_E_HIP;
     uint64_t off = 0;
     int rc = SRPC_OK;
@@ -157,8 +180,7 @@ int srpc_gather_wire(srpc_comm* c, const uint8_t* d_shard, uint64_t shard_bytes,
         }
         off += b;
     }
-    const int end = nccl_rc(ncclGroupEnd());
-    return rc ? rc : end;
+    return close_group(rc, &c, 1);
 }
 
 int srpc_group_gather_wire(srpc_comm* const* comms, int ndev, const uint8_t* const* d_shards,
@@ -166,8 +188,14 @@ int srpc_group_gather_wire(srpc_comm* const* comms, int ndev, const uint8_t* con
                            void* const* streams) {
     if (!comms || ndev <= 0 || !d_shards || !h_bytes || root < 0 || root >= ndev || !streams) return SRPC_E_INVALID;
     uint64_t total = 0;
-    for (int g = 0; g < ndev; ++g) total += h_bytes[g];
+    for (int g = 0; g < ndev; ++g) {
+        if (!comms[g] || !comms[g]->comm || comms[g]->nranks != ndev || comms[g]->rank != g) return SRPC_E_INVALID;
+        if (h_bytes[g] && !d_shards[g]) return SRPC_E_INVALID;
+        if (h_bytes[g] > ~0ull - total) return SRPC_E_INVALID;
+        total += h_bytes[g];
+    }
     if (total > root_cap) return SRPC_E_CAPACITY;
+    if (total && !d_root_wire) return SRPC_E_INVALID;
     // one group over every device's operations (a single process drives all ranks)
     if (ncclGroupStart() != ncclSuccess) return SRPC_E_HIP;
     int rc = SRPC_OK;
@@ -188,16 +216,21 @@ int srpc_group_gather_wire(srpc_comm* const* comms, int ndev, const uint8_t* con
         }
         off += b;
     }
-    const int end = nccl_rc(ncclGroupEnd());
-    return rc ? rc : end;
+    return close_group(rc, comms, ndev);
 }
 
 int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comms, int ndev,
                            const void* const* const* d_cols, uint64_t n, uint8_t* const* d_shard_wire,
                            uint8_t* d_root_wire, uint64_t root_cap, int root, void* const* streams) {
     if (!plans || !comms || ndev <= 0 || !d_cols || !d_shard_wire || !streams) return SRPC_E_INVALID;
+    if (root < 0 || root >= ndev) return SRPC_E_INVALID;
     uint64_t rb = 0;
     if (srpc_plan_record_bytes(plans[0], &rb) != SRPC_OK || rb == 0) return SRPC_E_INVALID;  // fixed schemas
+    if (n > ~0ull / rb) return SRPC_E_INVALID;
+    if (n * rb > root_cap) return SRPC_E_CAPACITY;
+    if (n && !d_root_wire) return SRPC_E_INVALID;
+    for (int g = 0; g < ndev; ++g)  // everything checked before the first shard is packed
+        if (!plans[g] || !comms[g] || !comms[g]->comm || !d_cols[g] || !d_shard_wire[g]) return SRPC_E_INVALID;
     std::vector<uint64_t> bytes(static_cast<size_t>(ndev));
     std::vector<const uint8_t*> shards(static_cast<size_t>(ndev));
     for (int g = 0; g < ndev; ++g) {

@@ -113,21 +113,38 @@ class NativeComm:
     def gather_wire(self, local, all_bytes, root: int = 0, out=None, stream=None):
         """Every rank: its packed shard (uint8 device tensor).  Root: returns the
         concatenation in rank order (``out`` or a new tensor); others None."""
-        import ctypes as C
-
         import torch
+
+        sizes = [int(b) for b in all_bytes]
+        if len(sizes) != self.nranks:
+            raise ValueError(f"{len(sizes)} shard sizes for {self.nranks} ranks")
+        total = sum(sizes)
+        if self.rank == root and out is None:
+            out = torch.empty(max(total, 1), dtype=torch.uint8, device=local.device)
+        self._gather(local, sizes[self.rank], out if self.rank == root else None,
+                     total if self.rank == root else 0, sizes, root, stream)
+        return out[:total] if self.rank == root else None
+
+    def _gather(self, local, shard_bytes, out, root_cap, sizes, root, stream) -> None:
+        """srpc_gather_wire of the C ABI: shard r lands at sum(sizes[:r]) of
+        the root's ``out``."""
+        import ctypes as C
 
         from . import _lib
         from .packer import _dptr, _stream
-        total = int(sum(all_bytes))
-        if self.rank == root and out is None:
-            out = torch.empty(max(total, 1), dtype=torch.uint8, device=local.device)
-        sizes = (C.c_uint64 * len(all_bytes))(*[int(b) for b in all_bytes])
-        _lib.check(_lib.lib().srpc_gather_wire(self._h, _dptr(local), int(all_bytes[self.rank]),
-                                               _dptr(out) if self.rank == root else None,
-                                               total if self.rank == root else 0, sizes, root,
+        h = (C.c_uint64 * len(sizes))(*sizes)
+        _lib.check(_lib.lib().srpc_gather_wire(self._h, _dptr(local) if shard_bytes else None, shard_bytes,
+                                               _dptr(out) if out is not None else None, root_cap, h, root,
                                                _stream(stream)), "srpc_gather_wire")
-        return out[:total] if self.rank == root else None
+
+    def info(self) -> dict:
+        """What the RCCL communicator itself reports (srpc_comm_rank)."""
+        import ctypes as C
+
+        from . import _lib
+        r, nr = C.c_int(), C.c_int()
+        _lib.check(_lib.lib().srpc_comm_rank(self._h, C.byref(r), C.byref(nr)), "srpc_comm_rank")
+        return {"rank": r.value, "nranks": nr.value, "device": self.device}
 
     def close(self) -> None:
         from . import _lib

@@ -39,6 +39,14 @@ def test_cpp_schema_limits_refused():
     assert "0 failed" in out and out.count("refused:") == 3
 
 
+def test_cpp_multi_gpu_api_compiles():
+    """sharded_packer<T>::request, pack_gather, comm / device_group moves:
+    instantiated and linked against libsrpc_gpu.so, not called (no GPU)."""
+    from srpc_amd import build
+    build.build()
+    assert "ok" in _run("multi_api_compile_test")
+
+
 @pytest.mark.gpu
 def test_cpp_gpu_batch_packer():
     torch = pytest.importorskip("torch")

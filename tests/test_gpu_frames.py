@@ -137,6 +137,31 @@ def test_rejects_bad_arguments(classifier):
     assert rc == srpc_amd._lib.SRPC_E_INVALID
 
 
+def test_offsets_past_the_buffer_are_unknown(classifier):
+    """Offsets that run backwards or past buf_len (a caller bug, not a peer
+    frame): those frames are UNKNOWN and no byte past the buffer is read --
+    frame 1 is exactly one square request long but ends past buf_len."""
+    pre = framed_request_prefix(METHODS[0][0], METHODS[0][1])
+    one = pre + b"\x07\x00\x00\x00"
+    buf = one * 4
+    L = len(one)
+    offs = np.array([0, L, 2 * L, L], np.uint32)
+    n, K = 4, len(METHODS)
+    d_buf = dev(np.frombuffer(buf, np.uint8))
+    d_offs = dev(offs)
+    d_cls, d_idx = empty(n + 16), empty(4 * K * n + 16)
+    d_counts, d_out_off = empty(8 * (K + 2)), empty(8 * (n + 1))
+    sb = classifier.scratch_bytes(n)
+    scratch = torch.empty(sb, dtype=torch.uint8, device="cuda:0")
+    # buf_len = 2L - 1 (the allocation holds four whole requests)
+    classifier.classify(d_buf, 2 * L - 1, d_offs, n, d_cls, d_idx, d_counts, d_out_off, scratch, sb)
+    # frame 0 [0, L): a square request; frame 1 [L, 2L): one request long but
+    # ends past buf_len; frame 2 [2L, L): backwards; frame 3 [L, 2L - 1): short
+    assert host(d_cls, n).tolist() == [0, UNKNOWN, UNKNOWN, UNKNOWN]
+    counts = host(d_counts, 8 * (K + 2), np.uint64)
+    assert int(counts[K + 1]) == 3 and int(counts[0]) == 1
+
+
 def test_sixteen_methods_one_body():
     """SRPC_FRAMES_MAX_PLANS plans of the same body size (frames differ only in
     the method name): every bucket gets exactly its frames."""
