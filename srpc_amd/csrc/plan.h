@@ -157,6 +157,33 @@ __device__ __forceinline__ uint64_t lds_u64(const uint8_t* lds, uint32_t off) {
     return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, s)) << 32) | __builtin_amdgcn_alignbyte(w1, w0, s);
 }
 
+// LDS bytes [s, s + len) -> LDS bytes [d, d + len): aligned dword stores in
+// the body, each built from two aligned dword loads of the source and a byte
+// funnel shift (the load may read up to 3 bytes past the run, inside the LDS
+// allocation, never used).
+__device__ __forceinline__ void lds_copy_run(uint8_t* lds, uint32_t d, uint32_t s, uint32_t len) {
+    while (len && (d & 3)) {
+        lds[d++] = lds[s++];
+        --len;
+    }
+    if (len >= 4) {
+        const uint32_t sa = s & 3;
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(lds + (s - sa));
+        uint32_t* dw = reinterpret_cast<uint32_t*>(lds + d);
+        const uint32_t nd = len >> 2;
+        uint32_t w0 = sw[0];
+        for (uint32_t k = 0; k < nd; ++k) {
+            const uint32_t w1 = sw[k + 1];
+            dw[k] = sa ? __builtin_amdgcn_alignbyte(w1, w0, sa) : w0;
+            w0 = w1;
+        }
+        d += 4 * nd;
+        s += 4 * nd;
+        len &= 3;
+    }
+    while (len--) lds[d++] = lds[s++];
+}
+
 }  // namespace srpc_impl
 
 // The object behind the opaque srpc_plan* of include/srpc_gpu.h.

@@ -22,10 +22,13 @@
 //    starts at 0.  By induction every chunk up to the first wrong one is
 //    right.
 // 3. repair rounds (k_stream_refix / k_stream_recheck, gated) walk the wrong
-//    chunks again from entries that are final; k_stream_fix (one thread,
-//    runs only if chunks are still wrong) walks the chunks from the first
-//    wrong one in order, each from its predecessor's corrected exit, until
-//    the stream stops; chunks whose start already agrees are kept.
+//    chunks again from entries that are final.  If chunks are still wrong
+//    after them (data on which a wrong start parses too: zero-heavy strings,
+//    records of zeros), k_stream_gate hands the stream to the single-pass
+//    decode of stream1.hip, whose work is bounded for any input (per-block
+//    candidate tables and a decoupled look-back, no serial walk over the
+//    stream); its kernels are launched on the same stream and return at once
+//    unless the gate is set.
 // 4. the chunks' record counts are scanned to record numbers, and
 //    k_stream_index copies each chunk's record starts into rec_offs[];
 //    k_stream_tail fills what the stream does not hold.
@@ -37,12 +40,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 
 #include "plan.h"
 #include "scan.h"
 #include "srpc_gpu.h"
+#include "stream1.h"
 
 
 namespace srpc_impl {
@@ -581,6 +586,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uin
         // that agrees -- runs of mis-speculated chunks (short records) are
         // repaired in one round instead of one chunk per round.  Every chunk
         // written and the chunks up to the next record start are rechecked.
+        // The walk stops before the next bad chunk: that one is another lane's
+        // (or a later round's), so no chunk is written by two lanes of a round
+        // (bad flags change only in k_stream_recheck).
         uint64_t ent = start != kNone ? exit : e;
         bool stp = start != kNone && stop != 0;
         uint64_t mb = ~0ull;
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_refix(StreamArgs a, const uin
                 atomicOr(&ch.blk[mb], kBlkRecheck);
             }
             const uint64_t hj = min((j + 1) * kChunk, W);
-            if (agrees(ent, hj, ch.start[j])) break;
+            if (ch.bad[j] || agrees(ent, hj, ch.start[j])) break;
             uint64_t cnt2 = 0, exit2 = kNone, start2 = kNone;
             uint32_t stop2 = 0;
             if (ent < hj) {
@@ -650,48 +658,17 @@ __global__ __launch_bounds__(kBlock) void k_stream_stop(uint64_t C, Chunks ch) {
         atomicMin(&ch.ctl[1], static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull)));
 }
 
-// One workgroup, thread 0, only when some chunk before the stream's stop is
-// bad: from the first bad chunk on, every chunk in order from its
-// predecessor's (corrected) exit until the stream stops.  Chunks that agree
-// are kept; 256-chunk blocks with no bad chunk and no stop are skipped.
-__global__ void k_stream_fix(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W, uint64_t C, Chunks ch) {
+// The hand-off: chunks still wrong before the stream's stop after the repair
+// rounds -> ctl[6] = 1, the single-pass decode (stream1.hip) runs (it is
+// bounded for any input; the round-2 one-thread in-order fixer here was not).
+// `force` (a test hook, srpc_debug_stream_force_single) hands every stream over.
+__global__ void k_stream_gate(Chunks ch, uint32_t force) {
     if (threadIdx.x != 0) return;
     uint32_t first;
-    if (!final_bad(ch, &first) || ch.ctl[1] < first) return;
-    ch.ctl[6] = 1;
-    uint64_t c = first;
-    while (c < C) {
-        const uint64_t hi = min((c + 1) * kChunk, W);
-        bool stopped;
-        const uint64_t e = entry_of(ch, c, &stopped);
-        if (stopped) {  // the stream stopped before chunk c (in a chunk already right)
-            return;
-        }
-        const bool fix = ch.bad[c] || !agrees(e, hi, ch.start[c]);
-        if (fix) {
-            uint64_t cnt = 0, exit = kNone, start = kNone;
-            uint32_t stop = 0;
-            if (e < hi) {
-                start = e;
-                walk(a, w, W, e, hi, &cnt, &exit, &stop, ch.list + c * ch.cap, ch.cap);
-            }
-            ch.start[c] = start;
-            ch.cnt[c] = cnt;
-            ch.exit[c] = exit;
-            ch.stop[c] = stop;
-            ch.bad[c] = 0;
-        }
-        if (ch.stop[c] && ch.start[c] != kNone) {
-            ch.ctl[1] = static_cast<uint32_t>(min<uint64_t>(c, 0xfffffffeull));
-            return;
-        }
-        ++c;
-        // skip blocks that hold neither a bad chunk nor a stop: they agree --
-        // unless this chunk was just corrected (the next block's first chunk
-        // was checked against its old exit)
-        while (!fix && c < C && (c & 255) == 0 && ch.blk[c >> 8] == 0) c += 256;
-    }
+    ch.ctl[6] = (force || (final_bad(ch, &first) && ch.ctl[1] >= first)) ? 1u : 0u;
 }
+
+std::atomic<uint32_t> g_force_single{0};
 
 // Records of chunk c that enter the index: none past the stream's stop chunk.
 __device__ __forceinline__ uint64_t chunk_count(const Chunks& ch, uint64_t c, uint64_t C, uint64_t stopc) {
@@ -777,9 +754,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_tail(uint64_t W, uint64_t C, 
 }
 
 // Diagnostic (srpc_unpack_status.reserved bit 0): some speculated chunk had
-// to be walked again.
+// to be walked again (the single pass adds its own bits, stream1.hip).
 __global__ void k_stream_note(const Chunks ch, srpc_unpack_status* st) {
-    if (threadIdx.x == 0 && (ch.ctl[5] || ch.ctl[6])) atomicOr(&st->reserved, 1u | (ch.ctl[6] ? 2u : 0u));
+    if (threadIdx.x == 0 && (ch.ctl[5] || ch.ctl[6])) atomicOr(&st->reserved, 1u);
 }
 
 __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
@@ -788,7 +765,7 @@ __global__ void k_stream_ctl_reset(Chunks ch, uint64_t nblk) {
         ch.ctl[1] = 0xffffffffu;  // the chunk where the stream stops
         ch.ctl[2] = 0xffffffffu;  // the first bad chunk
         ch.ctl[5] = 0;            // repair rounds run
-        ch.ctl[6] = 0;            // the serial fixer ran
+        ch.ctl[6] = 0;            // the single-pass decode takes over
         for (uint32_t r = 0; r < kRepairRounds; ++r) {
             ch.ctl[kCtlRound + 2 * r] = 0;                // round r: any bad
             ch.ctl[kCtlRound + 2 * r + 1] = 0xffffffffu;  // round r: first bad
@@ -843,7 +820,7 @@ int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t 
     if (!p || !out || !p->has_string) return SRPC_E_INVALID;
     uint64_t var = 0;
     if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
-    *out = r256(var) + stream_layout(wire_len, p->fixed_bytes).total;
+    *out = r256(var) + r256(stream_layout(wire_len, p->fixed_bytes).total) + stream1_scratch_bytes(p, wire_len);
     return SRPC_OK;
 }
 
@@ -892,7 +869,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
             launch(k_stream_recheck, dim3(gr), dim3(kBlock), 0, s, wire_len, C, ch, static_cast<uint32_t>(r));
         }
         launch(k_stream_stop, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch);
-        launch(k_stream_fix, dim3(1), dim3(64), 0, s, a, wire, wire_len, C, ch);
+        launch(k_stream_gate, dim3(1), dim3(64), 0, s, ch, g_force_single.load(std::memory_order_relaxed));
         launch(k_stream_count, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, C, ch, parts);
     }
     const uint64_t nb = wire_len ? g : 0;
@@ -903,14 +880,32 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     launch(k_stream_tail, dim3(static_cast<uint32_t>(std::min<uint64_t>(n / kBlock + 1, 4096))), dim3(kBlock), 0, s,
            wire_len, wire_len ? C : 0ull, ch, static_cast<const uint64_t*>(parts + g), n, rec_offs);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    // the single pass's scratch, and its gate (0 when the chunks settled or the
+    // wire is empty)
+    void* s1 = base + r256(L.total);
+    const uint32_t* gate = wire_len ? ch.ctl + 6 : nullptr;
+    const bool decodes = stream1_decodes(p);
+    if (wire_len && !decodes)  // more string fields than it carries: its index replaces ours
+        if (int rc = stream1_launch(p, wire, wire_len, n, rec_offs, cols, str_offs, st, s1, gate, s)) return rc;
     // the indexed decode over the index just built (the timing hook, if armed,
     // covers the index kernels above only)
     const int rc = srpc_gpu_unpack_var(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch, var, stream);
-    if (rc == SRPC_OK && st) {
+    if (rc != SRPC_OK) return rc;
+    if (wire_len && decodes)  // rewrites every output when the gate is set
+        if (int rc2 = stream1_launch(p, wire, wire_len, n, rec_offs, cols, str_offs, st, s1, gate, s)) return rc2;
+    if (st) {
         hipLaunchKernelGGL(k_stream_note, dim3(1), dim3(64), 0, s, ch, st);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+        if (wire_len) return stream1_note(p, wire_len, s1, st, gate, s);
     }
-    return rc;
+    return SRPC_OK;
 }
 
 }  // extern "C"
+
+// Test hook (not part of the C ABI in include/): 1 = every later stream decode
+// runs the single-pass kernels whatever the chunk pipeline found, 0 = only
+// when it leaves chunks wrong.  Returns the previous setting.
+extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_force_single(int on) {
+    return static_cast<int>(srpc_impl::g_force_single.exchange(on ? 1u : 0u));
+}

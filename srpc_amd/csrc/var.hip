@@ -1023,33 +1023,6 @@ constexpr uint64_t kRtuMinAvg = 40;  // record-tile unpack: smallest average rec
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
 typedef uint8_t __attribute__((address_space(3))) lds_u8;
 
-// LDS bytes [s, s + len) -> LDS bytes [d, d + len): aligned dword stores in
-// the body, each built from two aligned dword loads of the source and a byte
-// funnel shift (the load may read up to 3 bytes past the run, inside the LDS
-// allocation, never used).
-__device__ __forceinline__ void lds_copy_run(uint8_t* lds, uint32_t d, uint32_t s, uint32_t len) {
-    while (len && (d & 3)) {
-        lds[d++] = lds[s++];
-        --len;
-    }
-    if (len >= 4) {
-        const uint32_t sa = s & 3;
-        const uint32_t* sw = reinterpret_cast<const uint32_t*>(lds + (s - sa));
-        uint32_t* dw = reinterpret_cast<uint32_t*>(lds + d);
-        const uint32_t nd = len >> 2;
-        uint32_t w0 = sw[0];
-        for (uint32_t k = 0; k < nd; ++k) {
-            const uint32_t w1 = sw[k + 1];
-            dw[k] = sa ? __builtin_amdgcn_alignbyte(w1, w0, sa) : w0;
-            w0 = w1;
-        }
-        d += 4 * nd;
-        s += 4 * nd;
-        len &= 3;
-    }
-    while (len--) lds[d++] = lds[s++];
-}
-
 // A workgroup is resident for the whole batch and takes tiles t, t + G, ...
 // (G = the grid, sized by the host to what the chip holds at once), software
 // pipelined so that its loads and stores overlap instead of following each

@@ -5,12 +5,21 @@ record index.  Checked against the oracle's cursor (oracle/packer_oracle.c
 orc_unpack) and the reference-produced fixtures:
 - the reference's multiple_strings.bin (301 records, strings 0..300 bytes);
 - the packer_test.cpp vectors repeated 100,003 times;
-- random schemas, short and long strings (chunks inside one record pass
+- random schemas, short and long strings (blocks inside one record pass
   their entry on), and zero-heavy data on which the speculative starts are
-  often wrong (the in-order fixer then walks the chunks again);
+  often wrong (the chains are walked from every candidate of a block);
+- adversarial streams at scale (1M-4M records: zero-heavy strings, records
+  of zeros only, every phase of which parses), and long zero-filled strings
+  whose ends no block can guess (each such block waits for its predecessor);
 - streams cut short, foreign prefixes, fewer records than asked for, and
   trailing bytes after the n-th record.
+Tests taking the `path` fixture run twice: the chunk pipeline as it chooses
+("auto": the single pass only when chunks stay wrong after the repair
+rounds), and with every stream handed to the single-pass decode ("single",
+the srpc_debug_stream_force_single test hook), so both decoders meet the
+same cases.
 """
+import ctypes
 import json
 import os
 
@@ -28,6 +37,18 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
     pytest.skip("no GPU", allow_module_level=True)
 
 from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty, host, read_status, status_buf  # noqa: E402
+
+RES_ROUNDS, RES_SINGLE, RES_SINGLE_LEFT = 1, 2, 4  # srpc_unpack_status.reserved bits (srpc_gpu.h)
+
+
+@pytest.fixture(params=["auto", "single"])
+def path(request):
+    hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
+    hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
+    prev = hook(1 if request.param == "single" else 0)
+    yield request.param
+    hook(prev)
+
 
 GPU_OF_ORC = {oracle.ORC_ERR_BOUNDS: srpc_amd.SRPC_STATUS_BOUNDS, oracle.ORC_ERR_PREFIX: srpc_amd.SRPC_STATUS_PREFIX}
 
@@ -76,7 +97,7 @@ def check_clean(p, kinds, wire, n):
     return rec
 
 
-def test_reference_fixture_without_index(golden_dir):
+def test_reference_fixture_without_index(golden_dir, path):
     z = np.load(os.path.join(golden_dir, "multiple_strings_in.npz"))
     kinds = [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]
     p = GpuPacker(Schema("multiple_primitives", tuple((f"a{i}", k) for i, k in enumerate(kinds))))
@@ -88,7 +109,7 @@ def test_reference_fixture_without_index(golden_dir):
 
 @pytest.mark.parametrize("reps", [1, 100_003])
 @pytest.mark.parametrize("which", ["unpack request/multiple", "unpack response/nested"])
-def test_packer_test_vectors_repeated(which, reps):
+def test_packer_test_vectors_repeated(which, reps, path):
     with open(os.path.join(os.path.dirname(__file__), "golden", "packer_test_vectors.json")) as f:
         case = {c["section"]: c for c in json.load(f)}[which]
     one = bytes.fromhex(case["input"])
@@ -114,7 +135,7 @@ KINDS = {"s": [oracle.STRING],
 @pytest.mark.parametrize("schema,maxlen,envelope", [("s", 40, None), ("mixed", 300, None),
                                                     ("two_str", 16, "request"), ("s", 5000, None),
                                                     ("nested", 64, "response")])
-def test_random_streams(n, schema, maxlen, envelope):
+def test_random_streams(n, schema, maxlen, envelope, path):
     kinds = KINDS[schema]
     if maxlen > 1000 and n > 3000:
         n = 3000
@@ -126,16 +147,22 @@ def test_random_streams(n, schema, maxlen, envelope):
     wire = oracle.pack(kinds, cols, n, p.prefix, list(offs))
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
-    # random strings: the parallel repair rounds settle every mis-speculated
-    # chunk; the in-order fixer (one thread) is not needed
-    assert not stream_unpack.last_reserved & 2
+    r = stream_unpack.last_reserved
+    if path == "auto":  # random strings: the chunk pipeline settles, no hand-over
+        assert not r & RES_SINGLE, r
+    elif n:
+        # a single-pass block's entry is almost always one of its candidates
+        # (blocks that waited for their predecessor's state: bits 8-31)
+        blocks = (len(wire) + 8191) // 8192
+        assert r & RES_SINGLE and r >> 8 <= 1 + blocks // 20, (r >> 8, blocks)
 
 
 @pytest.mark.parametrize("n", [257, 20_000])
-def test_zero_heavy_streams_misspeculate_and_fix(n):
+def test_zero_heavy_streams_misspeculate_and_fix(n, path):
     """Zero bytes everywhere: a string length read at a wrong offset is often
-    0, so many chunks speculate a wrong start; the in-order fixer walks them
-    again.  The result must still be exact."""
+    0, so many chunks speculate a wrong start; the repair rounds walk them
+    again, and what they leave wrong goes to the single pass.  The result
+    must still be exact."""
     kinds = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
     rng = np.random.default_rng(n)
     cols, offs = [], []
@@ -157,7 +184,9 @@ def test_zero_heavy_streams_misspeculate_and_fix(n):
     wire = oracle.pack(kinds, cols, n, b"", list(offs))
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
-    assert stream_unpack.last_reserved & 1, "expected the fixer to run on zero-heavy data"
+    r = stream_unpack.last_reserved
+    assert r & RES_ROUNDS, "expected chains that leave the speculation on zero-heavy data"
+    assert (path == "single") <= bool(r & RES_SINGLE)
 
 
 def _error_case(p, kinds, wire, n):
@@ -176,7 +205,7 @@ def _error_case(p, kinds, wire, n):
             assert back[f][:err].tobytes() == ocols[f][:err].tobytes(), f
 
 
-def test_stream_errors():
+def test_stream_errors(path):
     kinds = KINDS["mixed"]
     n = 5000
     rng = np.random.default_rng(99)
@@ -200,7 +229,7 @@ def test_stream_errors():
     _error_case(p, kinds, wire, n + 7)
 
 
-def test_trailing_bytes_after_n_records():
+def test_trailing_bytes_after_n_records(path):
     kinds = KINDS["two_str"]
     n = 3000
     rng = np.random.default_rng(4)
@@ -217,7 +246,7 @@ def test_trailing_bytes_after_n_records():
 
 
 @pytest.mark.parametrize("prefix", [b"\x07", b"abc", b"1234567", b"12345678"])
-def test_short_custom_prefixes(prefix):
+def test_short_custom_prefixes(prefix, path):
     """Prefixes shorter than the 8-byte filter word (and exactly 8): the scan's
     prefix filter masks the bytes it compares; plausibility then needs two
     records (a bare or short prefix) or one (8 bytes or more)."""
@@ -226,6 +255,100 @@ def test_short_custom_prefixes(prefix):
     rng = np.random.default_rng(len(prefix))
     cols, offs = _random_string_batch(kinds, n, rng, 40)
     p = GpuPacker(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))), prefix)
+    wire = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
+
+
+def _zero_heavy(kinds, n, rng, maxlen=24, p_empty=0.5, p_nonzero=0.05):
+    cols, offs = [], []
+    for k in kinds:
+        if k == oracle.STRING:
+            lens = rng.integers(0, maxlen, n).astype(np.uint64)
+            lens[rng.random(n) < p_empty] = 0
+            o = np.zeros(n + 1, np.uint64)
+            o[1:] = np.cumsum(lens)
+            c = np.zeros(max(1, int(o[-1])), np.uint8)
+            c[rng.random(c.size) < p_nonzero] = 7
+            cols.append(c)
+            offs.append(o)
+        else:
+            cols.append(np.zeros(n, np.dtype(oracle.KIND_DTYPE[k])))
+            offs.append(None)
+    return cols, offs
+
+
+@pytest.mark.parametrize("n,schema", [(1 << 20, "zh4"), (1 << 22, "zh4"), (1 << 20, "zeros"), (1 << 22, "zeros")])
+def test_adversarial_streams_at_scale(n, schema, path):
+    """Streams on which a speculated start is usually wrong, at 1M-4M records:
+    zero-heavy strings (int8, string, int16, string), and records of zeros
+    only (multiple_primitives with empty strings: every one of its 18 phases
+    parses, to the end of the stream).  Checked against the oracle's cursor."""
+    rng = np.random.default_rng(n + len(schema))
+    if schema == "zh4":
+        kinds = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
+        cols, offs = _zero_heavy(kinds, n, rng)
+    else:
+        kinds = [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING]
+        cols, offs = _zero_heavy(kinds, n, rng, maxlen=1, p_empty=1.0, p_nonzero=0.0)
+    p = GpuPacker(Schema("Z", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    wire = oracle.pack(kinds, cols, n, b"", list(offs))
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
+
+
+@pytest.mark.parametrize("n", [300, 3000])
+def test_long_zero_strings_entries_no_block_guesses(n, path):
+    """Strings of 0-20000 zero bytes: inside one every position parses as an
+    empty record, so a block's candidates are all wrong and the record end
+    that enters it is found only from its predecessor's state (the miss path:
+    the block walks from its entry).  Exact, and each miss is counted."""
+    kinds = [oracle.STRING]
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 20000, n).astype(np.uint64)
+    o = np.zeros(n + 1, np.uint64)
+    o[1:] = np.cumsum(lens)
+    c = np.zeros(max(1, int(o[-1])), np.uint8)
+    p = GpuPacker(Schema("L", (("s", oracle.STRING),)))
+    wire = oracle.pack(kinds, [c], n, b"", [o])
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, [o], n))
+    r = stream_unpack.last_reserved
+    if r & RES_SINGLE:
+        assert r >> 8 > 0, r
+
+
+def test_records_across_block_edges_and_margin(path):
+    """Record lengths around the block (8 KiB) and its staged margin (2 KiB):
+    records that start in one block and end several blocks later, records
+    that run past the staged bytes (their tails read from global memory), one
+    record that covers a block exactly."""
+    kinds = [oracle.INT32, oracle.STRING, oracle.INT8]
+    lens = np.array([8192 - 21, 0, 2048, 2049, 2047, 8192, 8193, 16384 + 5, 3, 0, 7000, 9000, 1, 20000, 0, 5] * 7,
+                    np.uint64)
+    n = lens.size
+    rng = np.random.default_rng(5)
+    o = np.zeros(n + 1, np.uint64)
+    o[1:] = np.cumsum(lens)
+    chars = rng.integers(0, 256, int(o[-1]), dtype=np.uint8)
+    cols = [rng.integers(-2**31, 2**31, n).astype(np.int32), chars, rng.integers(-128, 128, n).astype(np.int8)]
+    p = GpuPacker(Schema("E", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    wire = oracle.pack(kinds, cols, n, b"", [None, o, None])
+    rec = check_clean(p, kinds, wire, n)
+    assert np.array_equal(rec, _rec_offsets(kinds, [None, o, None], n))
+
+
+@pytest.mark.parametrize("nstr", [3, 4, 5])
+def test_many_string_fields(nstr, path):
+    """Three and four string fields (the decode carries chars of all but the
+    last in its state), five (the record index, then the indexed decode)."""
+    kinds = []
+    for i in range(nstr):
+        kinds += [oracle.STRING, [oracle.INT8, oracle.INT16, oracle.INT64][i % 3]]
+    n = 20_011
+    rng = np.random.default_rng(nstr)
+    cols, offs = _random_string_batch(kinds, n, rng, 30)
+    p = GpuPacker.for_request(Schema("M", tuple((f"f{i}", k) for i, k in enumerate(kinds))), "Svc_servicer::many")
     wire = oracle.pack(kinds, cols, n, p.prefix, list(offs))
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
