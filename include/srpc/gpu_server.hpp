@@ -16,11 +16,20 @@
 //   frames) -> srpc_frames_scatter into request order -> D2H -> socket.
 //
 // A batch of one method skips the gather and scatter (its frames are already
-// the plan's contiguous records).  A frame no registered method matches
-// (another method, a string body, a corrupt header) is answered on the CPU
-// by an ordinary srpc::server, in its place in the reply order; only those
-// frames leave the GPU path.  A frame longer than the batch buffer is read on
-// its own and answered the same way.
+// the plan's contiguous records).  Methods with string fields
+// (register_var_method) take the variable-length form of each step:
+// srpc_frames_classify matches their frames by `str(method) | str(Req::name)`
+// after the BE32 and walks their fields to the frame's end;
+// srpc_frames_gather_var strips the BE32s and builds the record index ->
+// srpc_gpu_unpack_var -> the user's var handler (chars + offsets per string
+// field) -> srpc_gpu_pack_var -> srpc_frames_offsets (the reply stream's
+// offsets, now that the responses' sizes are known) ->
+// srpc_frames_scatter_var (`BE32 len | response` into request order).
+// A frame no registered method matches (another method, a corrupt header or
+// string length, trailing bytes) is answered on the CPU by an ordinary
+// srpc::server, in its place in the reply order; only those frames leave the
+// GPU path.  A frame longer than the batch buffer is read on its own and
+// answered the same way.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -98,6 +107,41 @@ std::vector<uint8_t> framed_response_prefix(rpc_status_code code) {
     return out;
 }
 
+/// Bytes of a record of T with every string empty (prefix excluded): the
+/// fixed leaves plus 8 (the length) per string.
+template <SrpcMessage T>
+uint64_t min_body_bytes() {
+    uint64_t s = 0;
+    T probe{};
+    for_each_leaf<T>(probe, [&](const auto& v) {
+        using F = std::remove_cvref_t<decltype(v)>;
+        s += std::is_same_v<F, std::string> ? 8 : sizeof(F);
+    });
+    return s;
+}
+
+/// A batch of a string-bodied method on the device, one entry per flattened
+/// field of Req / Resp: a fixed field is n values; a string field is its
+/// chars back to back (`*_cols[f]`) plus n+1 u64 offsets (`*_str_offs[f]`,
+/// nullptr for fixed fields) -- the layout of srpc_gpu_unpack_var /
+/// srpc_gpu_pack_var.  The handler writes every response column and the n+1
+/// offsets of every response string field (offs[0] need not be 0; at most
+/// resp_cap[f] chars).
+struct var_batch {
+    uint64_t n = 0;
+    void* const* req_cols = nullptr;
+    const uint64_t* const* req_str_offs = nullptr;
+    void* const* resp_cols = nullptr;
+    uint64_t* const* resp_str_offs = nullptr;
+    const uint64_t* resp_cap = nullptr;  // bytes of each response column
+};
+
+/// Sizing of a string-bodied method's buffers (per request of a batch).
+struct var_limits {
+    uint64_t max_request_bytes = 512;  // frame bytes the receive buffer is sized for
+    uint64_t max_response_chars = 256; // chars of one response's string field (batch average)
+};
+
 struct batch_stats {
     uint64_t requests = 0;           // frames answered
     uint64_t gpu_batches = 0;        // batches that went through the GPU path
@@ -120,6 +164,8 @@ public:
     /// handler(d_req_cols, d_resp_cols, n, stream): a method over a batch on
     /// the device (one column per flattened field of Req / Resp).
     using handler_t = std::function<int(void* const*, void* const*, uint64_t, hipStream_t)>;
+    /// handler(batch, stream) for a method with string fields (var_batch).
+    using var_handler_t = std::function<int(var_batch const&, hipStream_t)>;
 
     /// max_batch: frames per GPU batch; fallback: the CPU server for frames
     /// no registered method matches (nullptr: answered with
@@ -142,6 +188,7 @@ public:
     ~batch_server() {
         release();
         for (auto& m : _m) {
+            if (m->var) continue;  // released with the batch buffers
             for (void* p : m->req_cols) (void)hipFree(p);
             for (void* p : m->resp_cols) (void)hipFree(p);
         }
@@ -174,6 +221,46 @@ public:
         });
         _m.push_back(std::move(m));
         release();  // buffers are sized for the largest frames on the next serve
+    }
+
+    /// Serve `method` whose request and/or response has string fields: frames
+    /// `BE32 | str(method) | str(Req::name) | Req record`, answered with
+    /// `BE32 | RPC_SUCCESS | str(Resp::name) | Resp record` frames; `handler`
+    /// runs on whole batches of them (var_batch).  The receive buffer holds
+    /// max_batch frames of lim.max_request_bytes; longer frames still batch
+    /// while they fit, and one longer than the whole buffer is answered on
+    /// the CPU.  Up to SRPC_FRAMES_MAX_STRINGS string fields in Req.
+    template <SrpcMessage Req, SrpcMessage Resp>
+    void register_var_method(std::string method, var_handler_t handler, var_limits lim = {}) {
+        if (_m.size() >= SRPC_FRAMES_MAX_PLANS) throw plan_error("batch_server::register_var_method", SRPC_E_UNSUPPORTED);
+        check(hipSetDevice(_dev));
+        auto m = std::make_unique<method_entry>();
+        m->var = true;
+        m->name = std::move(method);
+        m->vhandler = std::move(handler);
+        const std::vector<uint8_t> rq = request_prefix<Req>(m->name), rs = response_prefix<Resp>(RPC_SUCCESS);
+        m->in = std::make_unique<raw_plan>(flat_kinds<Req>(), rq, _dev);
+        m->out = std::make_unique<raw_plan>(flat_kinds<Resp>(), rs, _dev);
+        m->req_prefix = rq;
+        m->min_in = rq.size() + min_body_bytes<Req>();
+        m->min_out = rs.size() + min_body_bytes<Resp>();
+        m->fin = std::max<uint64_t>(lim.max_request_bytes, 4 + m->min_in);
+        m->fout = 0;  // response frames vary
+        m->lim = lim;
+        Req rq0{};
+        for_each_leaf<Req>(rq0, [&](const auto& v) {
+            using F = std::remove_cvref_t<decltype(v)>;
+            m->req_string.push_back(std::is_same_v<F, std::string>);
+            m->req_size.push_back(std::is_same_v<F, std::string> ? 0 : sizeof(F));
+        });
+        Resp rs0{};
+        for_each_leaf<Resp>(rs0, [&](const auto& v) {
+            using F = std::remove_cvref_t<decltype(v)>;
+            m->resp_string.push_back(std::is_same_v<F, std::string>);
+            m->resp_size.push_back(std::is_same_v<F, std::string> ? 0 : sizeof(F));
+        });
+        _m.push_back(std::move(m));
+        release();
     }
 
     uint64_t request_frame_bytes(size_t k = 0) const { return _m.at(k)->fin; }
@@ -247,6 +334,19 @@ private:
         uint64_t fin = 0, fout = 0;
         std::vector<void*> req_cols, resp_cols;
         std::vector<uint64_t> req_bytes, resp_bytes;
+        // string-bodied methods (register_var_method); their device buffers are
+        // sized with the batch buffer (ensure / release)
+        bool var = false;
+        var_handler_t vhandler;
+        var_limits lim;
+        std::vector<uint8_t> req_prefix;           // str(method) | str(Req::name)
+        uint64_t min_in = 0, min_out = 0;          // records with empty strings
+        std::vector<bool> req_string, resp_string;
+        std::vector<uint64_t> req_size, resp_size;  // fixed leaves' bytes
+        std::vector<uint64_t*> req_offs, resp_offs; // string leaves' n+1 offsets (nullptr: fixed)
+        uint8_t* resp_wire = nullptr;               // packed responses and their index
+        uint64_t resp_wire_cap = 0;
+        uint64_t* resp_rec = nullptr;
     };
     void memset_cols(std::vector<void*> const& cols, std::vector<uint64_t> const& bytes) {
         for (size_t f = 0; f < cols.size(); ++f) check(hipMemsetAsync(cols[f], 0, bytes[f], _s));
@@ -281,19 +381,86 @@ private:
         for (auto const& m : _m) f = std::max(f, m->fout);
         return f;
     }
+    /// Bytes of a batch's reply stream: every frame of the widest fixed
+    /// response, plus every string method's framed responses.
+    uint64_t out_cap() const {
+        uint64_t c = _max * max_fout();
+        for (auto const& m : _m)
+            if (m->var) c += m->resp_wire_cap + 4 * _max;
+        return c;
+    }
+    bool any_var_method() const {
+        for (auto const& m : _m)
+            if (m->var) return true;
+        return false;
+    }
+
+    /// A string method's device buffers for batches of _max frames in _cap bytes.
+    void alloc_var(method_entry& m) {
+        m.req_cols.clear();
+        m.req_bytes.clear();
+        m.req_offs.clear();
+        for (size_t f = 0; f < m.req_string.size(); ++f) {
+            m.req_bytes.push_back(m.req_string[f] ? _cap + 16 : _max * m.req_size[f] + 16);
+            m.req_cols.push_back(alloc(m.req_bytes.back()));
+            m.req_offs.push_back(m.req_string[f] ? static_cast<uint64_t*>(alloc(8 * (_max + 1) + 16)) : nullptr);
+        }
+        m.resp_cols.clear();
+        m.resp_bytes.clear();
+        m.resp_offs.clear();
+        m.resp_wire_cap = _max * m.min_out + 16;
+        for (size_t f = 0; f < m.resp_string.size(); ++f) {
+            const uint64_t b = m.resp_string[f] ? _max * m.lim.max_response_chars + 16 : _max * m.resp_size[f] + 16;
+            if (m.resp_string[f]) m.resp_wire_cap += b;
+            m.resp_bytes.push_back(b);
+            m.resp_cols.push_back(alloc(b));
+            m.resp_offs.push_back(m.resp_string[f] ? static_cast<uint64_t*>(alloc(8 * (_max + 1) + 16)) : nullptr);
+        }
+        m.resp_wire = static_cast<uint8_t*>(alloc(m.resp_wire_cap));
+        m.resp_rec = static_cast<uint64_t*>(alloc(8 * (_max + 1) + 16));
+        uint64_t a = 0, b = 0;
+        check_srpc(srpc_plan_var_scratch_bytes(m.in->get(), _max, _cap, &a), "srpc_plan_var_scratch_bytes");
+        check_srpc(srpc_plan_var_scratch_bytes(m.out->get(), _max, m.resp_wire_cap, &b), "srpc_plan_var_scratch_bytes");
+        _var_scratch_bytes = std::max({_var_scratch_bytes, a, b});
+    }
+    void free_var(method_entry& m) {
+        for (void* p : m.req_cols) (void)hipFree(p);
+        for (void* p : m.resp_cols) (void)hipFree(p);
+        for (uint64_t* p : m.req_offs)
+            if (p) (void)hipFree(p);
+        for (uint64_t* p : m.resp_offs)
+            if (p) (void)hipFree(p);
+        if (m.resp_wire) (void)hipFree(m.resp_wire);
+        if (m.resp_rec) (void)hipFree(m.resp_rec);
+        m.req_cols.clear();
+        m.resp_cols.clear();
+        m.req_offs.clear();
+        m.resp_offs.clear();
+        m.resp_wire = nullptr;
+        m.resp_rec = nullptr;
+    }
 
     void ensure() {
         if (_h_in) return;
         const uint64_t K = _m.size();
         _cap = _max * max_fin();
         if (_cap > 0xffffffffull) throw plan_error("batch_server: batch buffer over 4 GiB", SRPC_E_UNSUPPORTED);
-        const uint64_t out_cap = _max * max_fout();
+        _var_scratch_bytes = 0;
+        for (auto& m : _m)
+            if (m->var) alloc_var(*m);
+        if (_var_scratch_bytes) _d_var_scratch = alloc(_var_scratch_bytes);
+        _d_pack_status = static_cast<srpc_unpack_status*>(alloc(sizeof(srpc_unpack_status)));
+        if (any_var_method()) {
+            _d_var_rec = alloc(8 * (_max + 1) + 16);
+            check(hipHostMalloc(reinterpret_cast<void**>(&_h_out_off), 8 * (_max + 1) + 16, hipHostMallocDefault));
+        }
+        const uint64_t out_cap = this->out_cap();
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_in), _cap + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_offs), 4 * _max + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_out), out_cap + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_cls), _max + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_counts), 8 * (K + 2) + 16, hipHostMallocDefault));
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_status), sizeof(srpc_unpack_status), hipHostMallocDefault));
+        check(hipHostMalloc(reinterpret_cast<void**>(&_h_status), 2 * sizeof(srpc_unpack_status), hipHostMallocDefault));
         check(hipMalloc(&_d_in, _cap + 16));
         check(hipMalloc(&_d_offs, 4 * _max + 16));
         check(hipMalloc(&_d_cls, _max + 16));
@@ -308,9 +475,13 @@ private:
         check(hipMalloc(&_d_scratch, _scratch_bytes));
         _in_plans.clear();
         _resp_bytes.clear();
+        _var_rec.clear();
+        _var_idx.clear();
         for (auto const& m : _m) {
+            if (m->var) _var_idx.push_back(_in_plans.size());
             _in_plans.push_back(m->in->get());
             _resp_bytes.push_back(static_cast<uint32_t>(m->fout));
+            _var_rec.push_back(m->var ? m->resp_rec : nullptr);
         }
         warm_up();
     }
@@ -321,7 +492,7 @@ private:
     /// on the connection's first batch (profiles/r02_e2e_warmup.log).
     void warm_up() {
         const int K = static_cast<int>(_m.size());
-        const uint64_t out_cap = _max * max_fout();
+        const uint64_t out_cap = this->out_cap();
         check(hipMemsetAsync(_d_out, 0, out_cap + 16, _s));
         check(hipMemsetAsync(_d_resp, 0, out_cap + 16, _s));
         check(hipMemsetAsync(_d_gather, 0, _cap + 16, _s));
@@ -332,7 +503,12 @@ private:
         for (auto const& m : _m) {
             memset_cols(m->req_cols, m->req_bytes);
             memset_cols(m->resp_cols, m->resp_bytes);
+            for (uint64_t* p : m->req_offs)
+                if (p) check(hipMemsetAsync(p, 0, 8 * (_max + 1), _s));
+            for (uint64_t* p : m->resp_offs)
+                if (p) check(hipMemsetAsync(p, 0, 8 * (_max + 1), _s));
         }
+        if (_d_var_scratch) check(hipMemsetAsync(_d_var_scratch, 0, _var_scratch_bytes, _s));
         std::memset(_h_in, 0, _cap);
         std::memset(_h_offs, 0, 4 * _max);
         // a batch's exact sequence of copies and launches on one all-zero frame,
@@ -349,6 +525,10 @@ private:
             check(hipStreamSynchronize(_s));
             check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
             for (auto const& m : _m) {
+                if (m->var) {
+                    warm_up_var(*m);
+                    continue;
+                }
                 check_srpc(srpc_frames_gather(static_cast<const uint8_t*>(_d_in), static_cast<const uint32_t*>(_d_offs),
                                               static_cast<const uint32_t*>(_d_index), 1, static_cast<uint32_t>(m->fin),
                                               static_cast<uint8_t*>(_d_gather), _s),
@@ -376,7 +556,57 @@ private:
             check(hipStreamSynchronize(_s));
         }
     }
+    /// One string-method batch on one well-formed request with empty strings
+    /// (its prefix, zeros): every kernel of the var path and the handler load
+    /// their code objects here, not on the first batch.
+    void warm_up_var(method_entry& m) {
+        std::vector<uint8_t> f = be32(static_cast<uint32_t>(m.min_in));
+        f.insert(f.end(), m.req_prefix.begin(), m.req_prefix.end());
+        f.resize(4 + m.min_in, 0);
+        check(hipMemcpyAsync(_d_in, f.data(), f.size(), hipMemcpyHostToDevice, _s));
+        check(hipMemsetAsync(_d_index, 0, 4, _s));
+        check(hipMemsetAsync(_d_offs, 0, 4, _s));
+        check_srpc(srpc_frames_gather_var(static_cast<const uint8_t*>(_d_in), static_cast<const uint32_t*>(_d_offs),
+                                          static_cast<const uint32_t*>(_d_index), 1, static_cast<uint8_t*>(_d_gather),
+                                          static_cast<uint64_t*>(_d_var_rec), _d_scratch, _scratch_bytes, _s),
+                   "srpc_frames_gather_var");
+        run_var_batch(m, 1, m.min_in);
+        check_srpc(srpc_frames_scatter_var(m.resp_wire, m.resp_rec, static_cast<const uint32_t*>(_d_index), 1,
+                                           static_cast<const uint64_t*>(_d_out_off), static_cast<uint8_t*>(_d_out), _s),
+                   "srpc_frames_scatter_var");
+    }
+    /// unpack_var -> handler -> pack_var over n gathered requests (_d_gather,
+    /// index _d_var_rec, at most wire_len bytes).
+    void run_var_batch(method_entry& m, uint64_t n, uint64_t wire_len) {
+        check_srpc(srpc_gpu_unpack_var(m.in->get(), static_cast<const uint8_t*>(_d_gather), wire_len, n,
+                                       static_cast<const uint64_t*>(_d_var_rec), m.req_cols.data(), m.req_offs.data(),
+                                       _d_status, _d_var_scratch, _var_scratch_bytes, _s),
+                   "srpc_gpu_unpack_var");
+        std::vector<const uint64_t*> req_offs(m.req_offs.begin(), m.req_offs.end());
+        var_batch b;
+        b.n = n;
+        b.req_cols = m.req_cols.data();
+        b.req_str_offs = req_offs.data();
+        b.resp_cols = m.resp_cols.data();
+        b.resp_str_offs = m.resp_offs.data();
+        b.resp_cap = m.resp_bytes.data();
+        check_srpc(m.vhandler(b, _s), "batch handler");
+        std::vector<const uint64_t*> resp_offs(m.resp_offs.begin(), m.resp_offs.end());
+        std::vector<const void*> resp_cols(m.resp_cols.begin(), m.resp_cols.end());
+        check_srpc(srpc_gpu_pack_var(m.out->get(), resp_cols.data(), resp_offs.data(), n, m.resp_wire, m.resp_wire_cap,
+                                     m.resp_rec, _d_pack_status, _d_var_scratch, _var_scratch_bytes, _s),
+                   "srpc_gpu_pack_var");
+    }
+
     void release() {
+        for (auto& m : _m)
+            if (m->var) free_var(*m);
+        for (void* p : {_d_var_rec, _d_var_scratch, static_cast<void*>(_d_pack_status)})
+            if (p) (void)hipFree(p);
+        if (_h_out_off) (void)hipHostFree(_h_out_off);
+        _d_var_rec = _d_var_scratch = nullptr;
+        _d_pack_status = nullptr;
+        _h_out_off = nullptr;
         for (void* p : {_d_in, _d_offs, _d_cls, _d_index, _d_counts, _d_out_off, _d_gather, _d_resp, _d_out,
                         static_cast<void*>(_d_status), _d_scratch})
             if (p) (void)hipFree(p);
@@ -413,17 +643,47 @@ private:
                                         _scratch_bytes, _s),
                    "srpc_frames_classify");
         check(hipMemcpyAsync(_h_counts, d_counts, 8 * (K + 2), hipMemcpyDeviceToHost, _s));
+        const bool var_methods = !_var_idx.empty();
+        if (var_methods) check(hipMemcpyAsync(_h_cls, _d_cls, nf, hipMemcpyDeviceToHost, _s));
         mark("classify");
         check(hipStreamSynchronize(_s));
         mark("sync1");
         st.classify_seconds += secs(t0);
-        const uint64_t total = _h_counts[K], unknown = _h_counts[K + 1];
-        bool mixed = false;
+        const uint64_t unknown = _h_counts[K + 1];
+        bool mixed = false, any_var = false;
+        for (int k = 0; k < K; ++k) any_var |= _m[static_cast<size_t>(k)]->var && _h_counts[k] > 0;
+        uint64_t var_bytes[SRPC_FRAMES_MAX_PLANS] = {};  // payload bytes of each string method's frames
+        if (any_var)
+            for (uint64_t i = 0; i < nf; ++i) {
+                const uint8_t c = _h_cls[i];
+                if (c != SRPC_FRAME_UNKNOWN && _m[c]->var) var_bytes[c] += (i + 1 < nf ? _h_offs[i + 1] : used) - _h_offs[i] - 4;
+            }
         check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
+        if (any_var) {
+            // string methods first: their responses' sizes place every answer
+            check(hipMemsetAsync(_d_pack_status, 0, sizeof(srpc_unpack_status), _s));
+            for (int k = 0; k < K; ++k) {
+                method_entry& m = *_m[static_cast<size_t>(k)];
+                const uint64_t n = _h_counts[k];
+                if (!m.var || !n) continue;
+                mixed |= n != nf;
+                check_srpc(srpc_frames_gather_var(d_in, d_offs, d_idx + static_cast<uint64_t>(k) * nf, n,
+                                                  static_cast<uint8_t*>(_d_gather), static_cast<uint64_t*>(_d_var_rec),
+                                                  _d_scratch, _scratch_bytes, _s),
+                           "srpc_frames_gather_var");
+                run_var_batch(m, n, var_bytes[k]);
+                mark("var batch");
+            }
+            check_srpc(srpc_frames_offsets(_in_plans.data(), _resp_bytes.data(), K, static_cast<const uint8_t*>(_d_cls),
+                                           nf, d_idx, d_counts, _var_rec.data(), d_out_off, d_counts + K, _d_scratch,
+                                           _scratch_bytes, _s),
+                       "srpc_frames_offsets");
+            check(hipMemcpyAsync(_h_counts + K, d_counts + K, 8, hipMemcpyDeviceToHost, _s));
+        }
         for (int k = 0; k < K; ++k) {
             const uint64_t n = _h_counts[k];
-            if (!n) continue;
             method_entry& m = *_m[static_cast<size_t>(k)];
+            if (!n || m.var) continue;
             const bool whole = n == nf;  // every frame is method k: they already are its contiguous records
             mixed |= !whole;
             const uint8_t* src = d_in;
@@ -447,21 +707,39 @@ private:
                                                _s),
                            "srpc_frames_scatter");
         }
+        if (any_var) {
+            for (int k = 0; k < K; ++k) {
+                method_entry& m = *_m[static_cast<size_t>(k)];
+                const uint64_t n = _h_counts[k];
+                if (m.var && n)
+                    check_srpc(srpc_frames_scatter_var(m.resp_wire, m.resp_rec, d_idx + static_cast<uint64_t>(k) * nf,
+                                                       n, d_out_off, static_cast<uint8_t*>(_d_out), _s),
+                               "srpc_frames_scatter_var");
+            }
+            check(hipMemcpyAsync(_h_status + 1, _d_pack_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
+            if (unknown) check(hipMemcpyAsync(_h_out_off, d_out_off, 8 * (nf + 1), hipMemcpyDeviceToHost, _s));
+            check(hipStreamSynchronize(_s));  // the reply stream's size
+            mark("sync_var");
+            if (_h_status[1].flags)
+                throw plan_error("batch_server: string responses exceed max_response_chars", SRPC_E_CAPACITY);
+        }
+        const uint64_t total = _h_counts[K];
         if (total) check(hipMemcpyAsync(_h_out, _d_out, total, hipMemcpyDeviceToHost, _s));
         mark("d2h_out");
-        if (unknown) check(hipMemcpyAsync(_h_cls, _d_cls, nf, hipMemcpyDeviceToHost, _s));
+        if (unknown && !var_methods) check(hipMemcpyAsync(_h_cls, _d_cls, nf, hipMemcpyDeviceToHost, _s));
         check(hipMemcpyAsync(_h_status, _d_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
         mark("d2h");
         check(hipStreamSynchronize(_s));
         mark("sync2");
-        // classification already matched every prefix and length: an unpack
-        // status here means the buckets and the plans disagree
+        // classification already matched every prefix and length (and walked
+        // string records to their frame's end): an unpack status here means
+        // the buckets and the plans disagree
         if (_h_status->flags) throw plan_error("batch_server: classified frame failed to unpack", SRPC_E_INVALID);
         const double dt = secs(t0);
         if (st.gpu_batches == 0 && st.fallback_requests == 0) st.first_batch_seconds = dt;
         st.gpu_seconds += dt;
         st.h2d_bytes += used + 4 * nf;
-        st.d2h_bytes += total + (unknown ? nf : 0);
+        st.d2h_bytes += total + (unknown || var_methods ? nf : 0) + (unknown && any_var ? 8 * (nf + 1) : 0);
         if (total) {
             st.gpu_batches += 1;
             st.mixed_batches += mixed ? 1 : 0;
@@ -482,7 +760,7 @@ private:
         for (uint64_t i = 0; i < nf; ++i) {
             const uint8_t c = _h_cls[i];
             if (c != SRPC_FRAME_UNKNOWN) {
-                run += _m[c]->fout;
+                run = any_var ? _h_out_off[i + 1] : run + _m[c]->fout;  // the end of frame i's answer
                 continue;
             }
             if (run > pos) _pieces.push_back({true, pos, run - pos});
@@ -594,6 +872,14 @@ private:
     void *_d_in = nullptr, *_d_offs = nullptr, *_d_cls = nullptr, *_d_index = nullptr, *_d_counts = nullptr,
          *_d_out_off = nullptr, *_d_gather = nullptr, *_d_resp = nullptr, *_d_out = nullptr, *_d_scratch = nullptr;
     srpc_unpack_status* _d_status = nullptr;
+    // string methods
+    std::vector<const uint64_t*> _var_rec;  // per method: its response index (nullptr: fixed)
+    std::vector<size_t> _var_idx;           // the string methods' slots
+    void* _d_var_rec = nullptr;             // the request index of the bucket being served
+    void* _d_var_scratch = nullptr;
+    uint64_t _var_scratch_bytes = 0;
+    srpc_unpack_status* _d_pack_status = nullptr;
+    uint64_t* _h_out_off = nullptr;
 };
 
 }  // namespace srpc::gpu

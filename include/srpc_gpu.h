@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 3
+#define SRPC_GPU_ABI_VERSION 4
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -302,10 +302,16 @@ int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comm
  * 58-69).  A batch read from a socket holds frames of any method in any order.
  * srpc_frames_classify puts frame i (bytes [d_offs[i], d_offs[i+1]) of d_buf,
  * the last frame ending at buf_len) into bucket k when it is exactly one record
- * of req_plans[k] -- a fixed-size plan whose prefix is the frame's constant
- * `BE32 len | str(method) | str(Req::name)`: same length, same prefix; the
- * first matching plan wins.  A frame whose offsets are out of order or run
- * past buf_len is SRPC_FRAME_UNKNOWN (no byte outside d_buf is read).
+ * of req_plans[k]; the first matching plan wins:
+ *   - a fixed-size plan whose prefix is the frame's constant
+ *     `BE32 len | str(method) | str(Req::name)`: same length, same prefix;
+ *   - a string plan (a method whose request has string fields; at most
+ *     SRPC_FRAMES_MAX_STRINGS of them) whose prefix is `str(method) |
+ *     str(Req::name)`: the frame's BE32 is its payload length, the payload
+ *     starts with the prefix and its fields, each string length read from
+ *     the frame, end exactly at the frame's end.
+ * A frame whose offsets are out of order or run past buf_len is
+ * SRPC_FRAME_UNKNOWN (no byte outside d_buf is read).
  * Outputs (device):
  *   d_class[i]             k, or SRPC_FRAME_UNKNOWN (the caller answers it);
  *   d_index[k*nframes + j] the frames of bucket k (j < d_counts[k]; order
@@ -314,11 +320,14 @@ int srpc_group_pack_gather(const srpc_plan* const* plans, srpc_comm* const* comm
  *                          bytes, then the number of unknown frames;
  *   d_out_off[0..nframes]  byte offset of frame i's response in the batch's
  *                          response stream (resp_bytes[k] per frame of bucket
- *                          k, 0 for unknown frames), total at [nframes].
+ *                          k, 0 for unknown frames and for string plans' frames,
+ *                          whose sizes srpc_frames_offsets adds), total at
+ *                          [nframes].
  * nplans <= SRPC_FRAMES_MAX_PLANS.  Scratch: srpc_frames_scratch_bytes, 8-byte
  * aligned.  Stream-ordered; nothing is synchronised. */
 #define SRPC_FRAME_UNKNOWN 0xFF
 #define SRPC_FRAMES_MAX_PLANS 16
+#define SRPC_FRAMES_MAX_STRINGS 16
 int srpc_frames_scratch_bytes(uint64_t nframes, int nplans, uint64_t* out);
 int srpc_frames_classify(const srpc_plan* const* req_plans, const uint32_t* resp_bytes, int nplans,
                          const uint8_t* d_buf, uint64_t buf_len, const uint32_t* d_offs,
@@ -331,6 +340,32 @@ int srpc_frames_gather(const uint8_t* d_buf, const uint32_t* d_offs, const uint3
 int srpc_frames_scatter(const uint8_t* d_resp, const uint32_t* d_index, uint64_t n,
                         uint32_t record_bytes, const uint64_t* d_out_off, uint8_t* d_out,
                         void* stream);
+/* String plans' buckets.  gather_var: the payloads (each frame after its BE32
+ * length) of frames d_index[0..n) back to back into d_out -- the records of a
+ * string request plan -- and their record index d_rec_offs[0..n] (n+1 u64) for
+ * srpc_gpu_unpack_var.  Frames must be ones srpc_frames_classify put in a
+ * string plan's bucket.  Scratch: srpc_frames_scratch_bytes(n, 1, ..). */
+int srpc_frames_gather_var(const uint8_t* d_buf, const uint32_t* d_offs, const uint32_t* d_index,
+                           uint64_t n, uint8_t* d_out, uint64_t* d_rec_offs, void* d_scratch,
+                           uint64_t scratch_bytes, void* stream);
+/* scatter_var: response j (bytes [d_rec_offs[j], d_rec_offs[j+1]) of d_resp, as
+ * srpc_gpu_pack_var wrote them with their index) framed as `BE32 len |
+ * response` at d_out + d_out_off[d_index[j]], j < n. */
+int srpc_frames_scatter_var(const uint8_t* d_resp, const uint64_t* d_rec_offs,
+                            const uint32_t* d_index, uint64_t n, const uint64_t* d_out_off,
+                            uint8_t* d_out, void* stream);
+/* The reply stream's offsets once string plans' responses are packed: frame i
+ * takes resp_bytes[k] (fixed plan k), 4 + its response's bytes (string plan k:
+ * d_var_rec_offs[k], a host array of nplans device pointers -- the index
+ * srpc_gpu_pack_var wrote for bucket k's records in d_index order; NULL for
+ * fixed plans), 0 (unknown).  Writes d_out_off[0..nframes] and *d_total.
+ * Same plans, d_class, d_index and d_counts as the classify call; same
+ * scratch size. */
+int srpc_frames_offsets(const srpc_plan* const* req_plans, const uint32_t* resp_bytes, int nplans,
+                        const uint8_t* d_class, uint64_t nframes, const uint32_t* d_index,
+                        const uint64_t* d_counts, const uint64_t* const* d_var_rec_offs,
+                        uint64_t* d_out_off, uint64_t* d_total, void* d_scratch,
+                        uint64_t scratch_bytes, void* stream);
 
 /* ---- utilities --------------------------------------------------------------*/
 

@@ -104,6 +104,7 @@ def ref_lib() -> C.CDLL:
             "ref_unpack_square_responses": (C.c_int, [_vp, _u64, _u64, _vp, _vp]),
             "ref_geo_locate_responses": (_u64, [_u64, _u64, _vp, _u64]),
             "ref_geo_locate_requests": (_u64, [_u64, _u64, _vp, _u64]),
+            "ref_server_echo": (_u64, [_u64, _vp, _u64, C.POINTER(_u64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

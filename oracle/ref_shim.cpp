@@ -30,6 +30,8 @@
 
 // deterministic Geo records shared with tests/cpp/batchgen_gpu_test.cpp
 #include "../tests/cpp/geo_records.hpp"
+// deterministic Echo requests shared with tools/e2e_square.hip --echo
+#include "../tests/cpp/echo_records.hpp"
 
 namespace {
 
@@ -171,6 +173,17 @@ struct Record : public srpc::message_base {
     void unpack(srpc::buffer::ptr) override {}
 };
 }  // namespace geo_ref
+
+// A service with a string-bodied method, declared the way the reference
+// generator emits a servicer (generator.hpp, calculator_srpc.cpp:63-83).
+struct Echo_servicer : srpc::servicer_base {
+    virtual multiple_primitives echo(multiple_primitives&) { throw std::runtime_error("Method not implemented!"); }
+    static constexpr const char* name = "Echo";
+    static constexpr auto methods = std::make_tuple(STRUCT_MEMBER(Echo_servicer, echo, "Echo_servicer::echo"));
+};
+struct EchoImpl : Echo_servicer {
+    multiple_primitives echo(multiple_primitives& q) override { return echo_fixture::answer(q); }
+};
 
 struct Calc : public Calculator_servicer {
     Number square(Number& req) override {
@@ -512,6 +525,37 @@ uint64_t ref_server_square(const uint8_t* reqs, uint64_t req_size, uint64_t n, u
         o += r->size();
     }
     if (secs) *secs = now_s() - t0;
+    return o;
+}
+
+// n Echo requests (echo_fixture::fill_request, pack_request with method
+// "Echo_servicer::echo") through the reference server one at a time, as
+// ref_server_square; *req_bytes = the request stream's bytes (unframed),
+// returns the response stream's bytes (unframed), written to out.
+uint64_t ref_server_echo(uint64_t n, uint8_t* out, uint64_t cap, uint64_t* req_bytes) {
+    register_all();
+    srpc::server s;
+    EchoImpl svc;
+    s.register_service(svc);
+    uint64_t o = 0, rq = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        multiple_primitives m;
+        echo_fixture::fill_request(m, i);
+        srpc::packer pr;
+        srpc::request_t<multiple_primitives> req;
+        req.set_method_name(echo_fixture::kMethod);
+        req.set_value(std::move(m));
+        pr.pack_request(req);
+        rq += pr.size();
+        srpc::packer::ptr p = std::make_shared<srpc::packer>(pr.data(), pr.size());
+        std::string funcname;
+        (*p) >> funcname;
+        srpc::packer::ptr r = s.call(funcname, p);
+        if (o + r->size() > cap) return UINT64_MAX;
+        std::memcpy(out + o, r->data(), r->size());
+        o += r->size();
+    }
+    if (req_bytes) *req_bytes = rq;
     return o;
 }
 

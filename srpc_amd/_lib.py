@@ -31,6 +31,7 @@ SRPC_MAX_FIELDS = 32
 SRPC_MAX_PREFIX = 1024
 SRPC_FRAMES_MAX_PLANS = 16
 SRPC_FRAME_UNKNOWN = 0xFF
+SRPC_FRAMES_MAX_STRINGS = 16
 
 SRPC_PATH_DWORD = 1
 SRPC_PATH_TILE = 2
@@ -70,6 +71,9 @@ SIGNATURES = {
                                        _vp]),
     "srpc_frames_gather": (C.c_int, [_vp, _vp, _vp, _u64, C.c_uint32, _vp, _vp]),
     "srpc_frames_scatter": (C.c_int, [_vp, _vp, _u64, C.c_uint32, _vp, _vp, _vp]),
+    "srpc_frames_gather_var": (C.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
+    "srpc_frames_scatter_var": (C.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "srpc_frames_offsets": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_status_string": (C.c_char_p, [C.c_int]),
     "srpc_gpu_abi_version": (C.c_int, []),
 }

@@ -330,6 +330,28 @@ class FrameClassifier:
         check(_lib.lib().srpc_frames_scatter(_dptr(resp), _dptr(index), n, record_bytes, _dptr(out_off),
                                              _dptr(out), _stream(stream)), "srpc_frames_scatter")
 
+    # string plans (request GpuPackers built with request_prefix, no BE32):
+    @staticmethod
+    def gather_var(buf, offs, index, n: int, out, rec_offs, scratch, scratch_bytes: int, stream=None) -> None:
+        check(_lib.lib().srpc_frames_gather_var(_dptr(buf), _dptr(offs), _dptr(index), n, _dptr(out), _dptr(rec_offs),
+                                                _dptr(scratch), scratch_bytes, _stream(stream)),
+              "srpc_frames_gather_var")
+
+    @staticmethod
+    def scatter_var(resp, rec_offs, index, n: int, out_off, out, stream=None) -> None:
+        check(_lib.lib().srpc_frames_scatter_var(_dptr(resp), _dptr(rec_offs), _dptr(index), n, _dptr(out_off),
+                                                 _dptr(out), _stream(stream)), "srpc_frames_scatter_var")
+
+    def offsets(self, cls, nframes: int, index, counts, var_rec_offs, out_off, total, scratch, scratch_bytes: int,
+                stream=None) -> None:
+        """var_rec_offs: per method, the response index of a string method's
+        bucket (device buffer) or None for a fixed one."""
+        k = len(self.methods)
+        vr = (C.c_void_p * k)(*[_dptr(v) if v is not None else None for v in var_rec_offs])
+        check(_lib.lib().srpc_frames_offsets(self._plans, self._rb, k, _dptr(cls), nframes, _dptr(index), _dptr(counts),
+                                             vr, _dptr(out_off), _dptr(total), _dptr(scratch), scratch_bytes,
+                                             _stream(stream)), "srpc_frames_offsets")
+
 
 __all__ = ["Schema", "GpuPacker", "SrpcError", "request_prefix", "response_prefix",
            "fill_splitmix_i32", "time_next_call", "framed_request_prefix", "framed_response_prefix",

@@ -107,3 +107,47 @@ def test_e2e_square_1M_reference_digest(manifest, tmp_path):
     with open(dump, "rb") as f:
         digest = hashlib.sha256(f.read()).hexdigest()
     assert digest == manifest["streams"]["square_responses_1M"]["sha256"]
+
+
+# ---- a string-bodied method (Echo_servicer::echo over multiple_primitives) ----
+def test_e2e_echo_string_method_all_on_the_gpu():
+    """Every request carries a string: classified, gathered with a record
+    index, unpacked, echoed, packed and framed on the GPU; the client checks
+    each answer byte for byte against the scalar packer's."""
+    n = 100_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "16384", "--port", "18321", "--echo", "1",
+             "--gpu-methods", "square,echo")
+    g = _served(r, n)
+    assert g["fallback_requests"] == 0 and g["gpu_requests"] == n and r["traffic"]["echo"] == n
+
+
+def test_e2e_echo_reference_digest(manifest, tmp_path):
+    """The unframed response stream of 200,000 echo requests equals the
+    reference server's (tests/golden/make_golden.py ref_server_echo)."""
+    want = manifest["streams"]["echo_responses"]
+    dump = str(tmp_path / "echo.bin")
+    r = _run("--mode", "gpu", "--n", str(want["records"]), "--batch", "65536", "--port", "18322", "--echo", "1",
+             "--gpu-methods", "echo", "--dump", dump)
+    assert _served(r, want["records"])["fallback_requests"] == 0
+    with open(dump, "rb") as f:
+        b = f.read()
+    assert len(b) == want["bytes"] and hashlib.sha256(b).hexdigest() == want["sha256"]
+
+
+def test_e2e_echo_mixed_with_fixed_methods_and_foreign_traffic():
+    """Echo, square, add/subtract/multiply on the GPU in one stream with 1 %
+    divide and three poisoned frames on the CPU: answers in request order."""
+    n = 120_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "32768", "--port", "18323", "--echo", "0.3", "--mix", "0.2",
+             "--foreign", "0.01", "--poison", "0,7,119999", "--gpu-methods", "all,echo")
+    g = _served(r, n)
+    t = r["traffic"]
+    assert t["echo"] > 30_000 and g["fallback_requests"] == t["divide"] + t["poison"]
+    assert g["mixed_batches"] >= 1
+
+
+def test_e2e_echo_on_the_cpu_when_not_registered():
+    n = 30_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "8192", "--port", "18324", "--echo", "0.25")
+    g = _served(r, n)
+    assert g["fallback_requests"] == r["traffic"]["echo"] > 5000

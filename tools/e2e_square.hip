@@ -20,7 +20,13 @@
 //                not have: answered by the CPU server in their places);
 //   --poison i[,j..]   requests with an unknown method name (NOT_REGISTERED);
 //   --poison-method    the name used (another length moves every later frame);
-//   --oversize i       request i has a method name longer than the batch buffer.
+//   --oversize i       request i has a method name longer than the batch buffer;
+//   --echo F     a fraction F of Echo_servicer::echo requests (multiple_primitives
+//                with a 0..40-byte string, tests/cpp/echo_records.hpp): a
+//                string-bodied method, on the GPU with --gpu-methods ...,echo
+//                (register_var_method), else on the CPU server; --echo 1
+//                --dump writes the unframed responses for the reference
+//                digest (tests/golden/manifest.json echo_responses).
 // Prints one JSON line.
 #include <hip/hip_runtime.h>
 #include <srpc/gpu_server.hpp>
@@ -37,6 +43,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include "../tests/cpp/echo_records.hpp"
 
 struct Number : public srpc::message_base {
     int32_t num;
@@ -61,7 +69,37 @@ struct TwoNumbers : public srpc::message_base {
     }
 };
 
-enum Op : int { SQUARE = 0, ADD = 1, SUB = 2, MUL = 3, DIV = 4, POISON = 5, OVERSIZE = 6 };
+// The reference packer test's message with a string (packer_test.cpp:26-45).
+struct multiple_primitives : public srpc::message_base {
+    int8_t arg1;
+    char arg2;
+    int64_t arg3;
+    std::string arg4;
+    static constexpr const char* name = "multiple_primitives";
+    static constexpr auto fields =
+        std::make_tuple(STRUCT_MEMBER(multiple_primitives, arg1, "multiple_primitives::arg1"),
+                        STRUCT_MEMBER(multiple_primitives, arg2, "multiple_primitives::arg2"),
+                        STRUCT_MEMBER(multiple_primitives, arg3, "multiple_primitives::arg3"),
+                        STRUCT_MEMBER(multiple_primitives, arg4, "multiple_primitives::arg4"));
+    void unpack(srpc::buffer::ptr bp) override {
+        srpc::packer p(bp);
+        p >> arg1;
+        p >> arg2;
+        p >> arg3;
+        p >> arg4;
+    }
+};
+
+struct Echo_servicer : srpc::servicer_base {
+    virtual multiple_primitives echo(multiple_primitives&) { throw std::runtime_error("Method not implemented!"); }
+    static constexpr const char* name = "Echo";
+    static constexpr auto methods = std::make_tuple(STRUCT_MEMBER(Echo_servicer, echo, "Echo_servicer::echo"));
+};
+struct EchoImpl : Echo_servicer {
+    multiple_primitives echo(multiple_primitives& q) override { return echo_fixture::answer(q); }
+};
+
+enum Op : int { SQUARE = 0, ADD = 1, SUB = 2, MUL = 3, DIV = 4, POISON = 5, OVERSIZE = 6, ECHO = 7 };
 
 static int32_t expect(int op, int32_t l, int32_t r) {
     const uint32_t a = static_cast<uint32_t>(l), b = static_cast<uint32_t>(r);
@@ -137,6 +175,36 @@ static int binop_batch(void* const* req, void* const* resp, uint64_t n, hipStrea
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// Echo on the device: ints + 1, each string with "!" appended (response
+// string i starts at req_offs[i] - req_offs[0] + i).  A thread per record.
+__global__ void k_echo(const int8_t* a1, const int8_t* a2, const int64_t* a3, const uint8_t* chars,
+                       const uint64_t* offs, int8_t* r1, int8_t* r2, int64_t* r3, uint8_t* rchars, uint64_t* roffs,
+                       uint64_t n, uint64_t cap) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const uint64_t o0 = offs[0];
+    roffs[i] = offs[i] - o0 + i;
+    if (i == n) return;
+    r1[i] = static_cast<int8_t>(static_cast<uint8_t>(a1[i]) + 1u);
+    r2[i] = static_cast<int8_t>(static_cast<uint8_t>(a2[i]) + 1u);
+    r3[i] = static_cast<int64_t>(static_cast<uint64_t>(a3[i]) + 1u);
+    const uint64_t b = offs[i], e = offs[i + 1], d = offs[i] - o0 + i;
+    if (d + (e - b) + 1 > cap) return;  // past the response column: pack_var reports it
+    for (uint64_t k = 0; k < e - b; ++k) rchars[d + k] = chars[b + k];
+    rchars[d + (e - b)] = '!';
+}
+
+static int echo_batch(srpc::gpu::var_batch const& b, hipStream_t s) {
+    const uint64_t blocks = (b.n + 1 + 255) / 256;
+    hipLaunchKernelGGL(k_echo, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
+                       static_cast<const int8_t*>(b.req_cols[0]), static_cast<const int8_t*>(b.req_cols[1]),
+                       static_cast<const int64_t*>(b.req_cols[2]), static_cast<const uint8_t*>(b.req_cols[3]),
+                       b.req_str_offs[3], static_cast<int8_t*>(b.resp_cols[0]), static_cast<int8_t*>(b.resp_cols[1]),
+                       static_cast<int64_t*>(b.resp_cols[2]), static_cast<uint8_t*>(b.resp_cols[3]), b.resp_str_offs[3],
+                       b.n, b.resp_cap[3]);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 static uint64_t splitmix(uint64_t* s) {
     uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -164,7 +232,7 @@ int main(int argc, char** argv) {
     std::set<uint64_t> poison;
     std::string poison_method = "Calculator_servicer::squarX";  // same frame length as square's
     int64_t oversize = -1;
-    double mix = 0, foreign = 0;
+    double mix = 0, foreign = 0, echo = 0;
     int watchdog_s = 60;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -181,6 +249,7 @@ int main(int argc, char** argv) {
         else if (a == "--oversize") oversize = std::stoll(next());
         else if (a == "--mix") mix = std::stod(next());
         else if (a == "--foreign") foreign = std::stod(next());
+        else if (a == "--echo") echo = std::stod(next());
         else if (a == "--gpu-methods") gpu_methods = next();
         else if (a == "--watchdog") watchdog_s = std::stoi(next());
     }
@@ -188,17 +257,24 @@ int main(int argc, char** argv) {
     srpc::message_registry["TwoNumbers"] = []() -> std::unique_ptr<TwoNumbers> {
         return std::make_unique<TwoNumbers>();
     };
+    srpc::message_registry["multiple_primitives"] = []() -> std::unique_ptr<multiple_primitives> {
+        return std::make_unique<multiple_primitives>();
+    };
 
     // ---- server ------------------------------------------------------------
     Calculator calc;
+    EchoImpl echo_svc;
     srpc::server cpu_server;
     cpu_server.register_service(calc);
+    cpu_server.register_service(echo_svc);
     std::unique_ptr<srpc::gpu::batch_server> gsrv;
     uint64_t buffer_bytes = 0;
     if (mode == "gpu") {
         gsrv = srpc::gpu::batch_server::single<Number, Number>("Calculator_servicer::square", square_batch, batch, 0,
                                                                &cpu_server);
-        if (gpu_methods == "all") {
+        if (gpu_methods.find("echo") != std::string::npos)
+            gsrv->register_var_method<multiple_primitives, multiple_primitives>(echo_fixture::kMethod, echo_batch);
+        if (gpu_methods.find("all") != std::string::npos) {
             gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::add", binop_batch<ADD>);
             gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::subtract", binop_batch<SUB>);
             gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::multiply", binop_batch<MUL>);
@@ -215,7 +291,8 @@ int main(int argc, char** argv) {
         lhs[i] = v % 46341;
         const double u = static_cast<double>(splitmix(&st2) >> 11) * 0x1.0p-53;
         const uint64_t w = splitmix(&st2);
-        ops[i] = u < foreign ? DIV : u < foreign + mix ? static_cast<uint8_t>(ADD + w % 3) : SQUARE;
+        ops[i] = u < foreign ? DIV : u < foreign + mix ? static_cast<uint8_t>(ADD + w % 3)
+                 : u < foreign + mix + echo ? ECHO : SQUARE;
         rhs[i] = ops[i] == DIV ? static_cast<int32_t>(w >> 40) % 1000 + 1 : static_cast<int32_t>(w >> 32);
         if (poison.count(i)) ops[i] = POISON;
         if (static_cast<int64_t>(i) == oversize) ops[i] = OVERSIZE;
@@ -225,11 +302,29 @@ int main(int argc, char** argv) {
                                   "Calculator_servicer::divide"};
     std::vector<uint8_t> frames;
     frames.reserve(n * 62);
-    uint64_t counts[7] = {};
+    uint64_t counts[8] = {};
     uint64_t resp_total = 0;
+    std::vector<uint8_t> echo_resp;      // the expected echo answers, framed, in request order
+    std::vector<uint64_t> echo_at(n, 0);  // where request i's answer starts in echo_resp
     for (uint64_t i = 0; i < n; ++i) {
         const int op = ops[i];
         counts[op] += 1;
+        if (op == ECHO) {
+            multiple_primitives q;
+            echo_fixture::fill_request(q, i);
+            srpc::packer pr;
+            srpc::response_t<multiple_primitives> r;
+            r.set_value(echo_fixture::answer(q));
+            pr.pack_response(r);
+            const uint32_t len = htonl(static_cast<uint32_t>(pr.size()));
+            const uint8_t* lb = reinterpret_cast<const uint8_t*>(&len);
+            echo_at[i] = echo_resp.size();
+            echo_resp.insert(echo_resp.end(), lb, lb + 4);
+            echo_resp.insert(echo_resp.end(), pr.data(), pr.data() + pr.size());
+            resp_total += 4 + pr.size();
+            append_frame(frames, echo_fixture::kMethod, std::move(q));
+            continue;
+        }
         if (op == SQUARE || op == POISON) {
             Number v;
             v.num = lhs[i];
@@ -323,6 +418,16 @@ int main(int argc, char** argv) {
     const uint8_t* f = resp.data();
     for (uint64_t i = 0; got_all && i < n; ++i) {
         const uint32_t len = (uint32_t(f[0]) << 24) | (uint32_t(f[1]) << 16) | (uint32_t(f[2]) << 8) | f[3];
+        if (ops[i] == ECHO) {  // byte for byte the scalar packer's framed answer
+            const uint8_t* e = echo_resp.data() + echo_at[i];
+            const uint64_t el = 4 + ((uint64_t(e[0]) << 24) | (uint64_t(e[1]) << 16) | (uint64_t(e[2]) << 8) | e[3]);
+            if (std::memcmp(f, e, el) != 0) {
+                ++bad;
+                break;
+            }
+            f += el;
+            continue;
+        }
         if (ops[i] == POISON || ops[i] == OVERSIZE) {
             if (len != 1 || f[4] != srpc::RPC_ERR_FUNCTION_NOT_REGISTERED) ++bad;
             f += 5;
@@ -337,10 +442,15 @@ int main(int argc, char** argv) {
         srpc::response_t<Number> m = rpr.unpack_response<Number>();
         if (m.code() != srpc::RPC_SUCCESS || m.value().num != expect(ops[i], lhs[i], rhs[i])) ++bad;
     }
-    const bool pure = poison.empty() && oversize < 0 && counts[SQUARE] == n;
+    const bool pure = poison.empty() && oversize < 0 && (counts[SQUARE] == n || counts[ECHO] == n);
     if (!dump.empty() && got_all && pure) {  // unframed responses, for the reference digest
         FILE* fp = std::fopen(dump.c_str(), "wb");
-        for (uint64_t i = 0; fp && i < n; ++i) std::fwrite(resp.data() + i * 23 + 4, 1, 19, fp);
+        const uint8_t* q = resp.data();
+        for (uint64_t i = 0; fp && i < n; ++i) {
+            const uint32_t len = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | q[3];
+            std::fwrite(q + 4, 1, len, fp);
+            q += 4 + len;
+        }
         if (fp) std::fclose(fp);
     }
     std::printf(
@@ -348,7 +458,7 @@ int main(int argc, char** argv) {
         "\"requests\": %llu, \"ok\": %s, \"bad\": %llu, \"seconds\": %.6f, \"requests_per_s\": %.1f, "
         "\"request_bytes\": %zu, \"wire_in_MBps\": %.1f, "
         "\"traffic\": {\"square\": %llu, \"add\": %llu, \"subtract\": %llu, \"multiply\": %llu, \"divide\": %llu, "
-        "\"poison\": %llu, \"oversize\": %llu, \"mix\": %.4f, \"foreign\": %.4f, \"gpu_methods\": \"%s\"}, "
+        "\"poison\": %llu, \"oversize\": %llu, \"echo\": %llu, \"mix\": %.4f, \"foreign\": %.4f, \"gpu_methods\": \"%s\"}, "
         "\"gpu\": {\"batches\": %llu, \"mixed_batches\": %llu, \"batch_frames\": %llu, \"buffer_bytes\": %llu, "
         "\"gpu_requests\": %llu, \"fallback_requests\": %llu, \"oversize_requests\": %llu, "
         "\"gpu_seconds\": %.6f, \"classify_seconds\": %.6f, \"first_batch_seconds\": %.6f, \"fallback_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, "
@@ -356,7 +466,8 @@ int main(int argc, char** argv) {
         mode.c_str(), (unsigned long long)n, (got_all && bad == 0) ? "true" : "false", (unsigned long long)bad, secs,
         n / secs, frames.size(), frames.size() / secs / 1e6, (unsigned long long)counts[SQUARE],
         (unsigned long long)counts[ADD], (unsigned long long)counts[SUB], (unsigned long long)counts[MUL],
-        (unsigned long long)counts[DIV], (unsigned long long)counts[POISON], (unsigned long long)counts[OVERSIZE], mix,
+        (unsigned long long)counts[DIV], (unsigned long long)counts[POISON], (unsigned long long)counts[OVERSIZE],
+        (unsigned long long)counts[ECHO], mix,
         foreign, gpu_methods.c_str(), (unsigned long long)stats.gpu_batches, (unsigned long long)stats.mixed_batches,
         (unsigned long long)batch, (unsigned long long)buffer_bytes, (unsigned long long)stats.gpu_requests,
         (unsigned long long)stats.fallback_requests, (unsigned long long)stats.oversize_requests, stats.gpu_seconds,
