@@ -12,14 +12,25 @@
 // device copy of the array (everything else -- vtable pointer, padding --
 // stays as the copy brought it), which the caller copies back.
 //
-// Kernels: a workgroup owns a tile of R records (the plan's TILE tiling), one
-// struct per lane: fields straight between the struct array and an LDS image
-// of the tile's wire bytes, which moves to / from HBM in 16-byte pieces with
-// the envelope prefix applied / checked from the plan's periodic template.
+// Kernels (struct array 16-byte aligned, the usual case): a workgroup owns a
+// tile of R records (R a multiple of 16, so the tile's struct bytes are whole
+// 16-byte pieces).  Both the tile's struct bytes and its wire bytes move
+// between HBM and LDS in coalesced 16-byte pieces; the fields move between
+// the two LDS images, one struct per lane.  Pack: structs -> LDS, fields ->
+// wire image, wire image (+ the envelope prefix from the plan's periodic
+// template) -> HBM.  Unpack: wire -> LDS (prefix checked), fields -> struct
+// image, struct image -> HBM; when the leaf fields do not cover every byte of
+// the struct (padding, a vtable pointer) the struct tile is read first so
+// those bytes are written back unchanged.  When the struct's layout is the
+// wire body's (same offsets and stride, no prefix -- e.g. Quad) the two images
+// are one and the kernels are tile copies.  A struct array that is only
+// naturally aligned takes the per-field kernels (one struct per lane, fields
+// straight between HBM and the wire image).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "plan.h"
 #include "srpc_gpu.h"
@@ -33,6 +44,9 @@ struct AosArgs {
     uint32_t woff[kMaxFields];  // offset inside the wire record (prefix included)
     const uint8_t* period;      // template | mask of one period (prefix_len > 0)
     uint32_t nfields, wstride, rstride, prefix_len, R, L;
+    uint32_t simg;              // staged kernels: LDS offset of the struct image (0: the wire image's, ident)
+    bool ident;                 // struct layout == wire layout
+    bool cover;                 // the leaf fields cover every byte of the struct
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -139,6 +153,136 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos(AosArgs a, const uint8_t*
     }
 }
 
+// HBM bytes [0, bytes) of a tile -> LDS (16-byte pieces, then single bytes).
+__device__ __forceinline__ void tile_in(uint8_t* lds, const uint8_t* __restrict__ g, uint32_t bytes) {
+    const uint32_t full = bytes >> 4;
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock)
+        reinterpret_cast<v4u*>(lds)[c] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g) + c);
+    for (uint32_t i = full * 16 + threadIdx.x; i < bytes; i += kBlock) lds[i] = g[i];
+}
+
+// LDS -> HBM bytes [0, bytes) of a tile.
+__device__ __forceinline__ void tile_out(uint8_t* __restrict__ g, const uint8_t* lds, uint32_t bytes) {
+    const uint32_t full = bytes >> 4;
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+        const uint4 v = reinterpret_cast<const uint4*>(lds)[c];
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + 16 * c));
+    }
+    for (uint32_t i = full * 16 + threadIdx.x; i < bytes; i += kBlock) g[i] = lds[i];
+}
+
+// Wire image (+ prefix template) -> wire, aligned 16-byte stores.
+__device__ __forceinline__ void wire_out(const AosArgs& a, const uint8_t* img, const uint8_t* tmpl, const uint8_t* mask,
+                                         uint8_t* __restrict__ dst, uint32_t tbytes) {
+    const uint32_t full = tbytes >> 4;
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+        uint4 v = reinterpret_cast<const uint4*>(img)[c];
+        if (a.prefix_len) {
+            const uint32_t ph = (16 * c) % a.L;
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + ph), t = *reinterpret_cast<const uint4*>(tmpl + ph);
+            v = make_uint4((v.x & ~m.x) | t.x, (v.y & ~m.y) | t.y, (v.z & ~m.z) | t.z, (v.w & ~m.w) | t.w);
+        }
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(dst + 16 * c));
+    }
+    for (uint32_t i = full * 16 + threadIdx.x; i < tbytes; i += kBlock) {
+        const uint32_t ph = i % a.L;
+        dst[i] = a.prefix_len && mask[ph] ? tmpl[ph] : img[i];
+    }
+}
+
+// Wire -> wire image, every prefix byte checked against the template.
+__device__ __forceinline__ void wire_in(const AosArgs& a, uint8_t* img, const uint8_t* tmpl, const uint8_t* mask,
+                                        const uint8_t* __restrict__ src, uint32_t tbytes, uint64_t rbase,
+                                        srpc_unpack_status* st) {
+    const uint32_t full = tbytes >> 4;
+    for (uint32_t c = threadIdx.x; c < full; c += kBlock) {
+        const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + c);
+        const uint4 v = make_uint4(w.x, w.y, w.z, w.w);
+        if (a.prefix_len && st) {
+            const uint32_t ph = (16 * c) % a.L;
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + ph), t = *reinterpret_cast<const uint4*>(tmpl + ph);
+            const uint32_t d[4] = {(v.x & m.x) ^ t.x, (v.y & m.y) ^ t.y, (v.z & m.z) ^ t.z, (v.w & m.w) ^ t.w};
+            for (uint32_t w = 0; w < 4; ++w)
+                if (d[w]) {
+                    const uint32_t i = 16 * c + 4 * w + (__builtin_ctz(d[w]) >> 3);
+                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.wstride);
+                    break;
+                }
+        }
+        reinterpret_cast<uint4*>(img)[c] = v;
+    }
+    for (uint32_t i = full * 16 + threadIdx.x; i < tbytes; i += kBlock) {
+        const uint8_t b = src[i];
+        const uint32_t ph = i % a.L;
+        if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph]) report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.wstride);
+        img[i] = b;
+    }
+}
+
+// LDS: wire image (R * wstride, 16-byte rounded) | struct image at a.simg
+// (unless ident) | template | mask.
+__global__ __launch_bounds__(kBlock) void k_pack_aos_staged(AosArgs a, const uint8_t* __restrict__ recs,
+                                                            uint8_t* __restrict__ wire, uint64_t n, uint32_t tmpl_at) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* tmpl = lds + tmpl_at;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) load_period(a, tmpl);
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    uint8_t* simg = lds + a.simg;
+    tile_in(simg, recs + rbase * a.rstride, nr * a.rstride);
+    __syncthreads();
+    if (!a.ident) {
+        for (uint32_t e = threadIdx.x; e < nr; e += kBlock) {
+            const uint8_t* src = simg + e * a.rstride;
+            const uint32_t d = e * a.wstride;
+            for (uint32_t f = 0; f < a.nfields; ++f)
+                lds_put_small(lds, d + a.woff[f], load_field(src + a.roff[f], a.size[f]), a.size[f]);
+        }
+        __syncthreads();
+    }
+    wire_out(a, lds, tmpl, mask, wire + rbase * a.wstride, nr * a.wstride);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_aos_staged(AosArgs a, const uint8_t* __restrict__ wire,
+                                                              uint8_t* __restrict__ recs, uint64_t n,
+                                                              srpc_unpack_status* st, uint32_t tmpl_at) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* tmpl = lds + tmpl_at;
+    uint8_t* mask = tmpl + a.L;
+    if (a.prefix_len) load_period(a, tmpl);
+    const uint64_t rbase = static_cast<uint64_t>(blockIdx.x) * a.R;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
+    uint8_t* simg = lds + a.simg;
+    uint8_t* g = recs + rbase * a.rstride;
+    if (!a.ident && !a.cover) tile_in(simg, g, nr * a.rstride);  // bytes no field covers are written back as they were
+    __syncthreads();  // the template, before wire_in reads it
+    wire_in(a, lds, tmpl, mask, wire + rbase * a.wstride, nr * a.wstride, rbase, st);
+    __syncthreads();
+    if (!a.ident) {
+        for (uint32_t e = threadIdx.x; e < nr; e += kBlock) {
+            uint8_t* dst = simg + e * a.rstride;
+            const uint32_t s = e * a.wstride;
+            for (uint32_t f = 0; f < a.nfields; ++f) store_field(dst + a.roff[f], lds_u64(lds, s + a.woff[f]), a.size[f]);
+        }
+        __syncthreads();
+    }
+    tile_out(g, simg, nr * a.rstride);
+}
+
+// Staged-kernel tiling: R (a multiple of 16) records whose two images fill
+// about kAosTileBytes of LDS; returns the LDS bytes, sets a->R / a->simg.
+constexpr uint32_t kAosTileBytes = 24 * 1024;
+uint32_t staged_tiling(AosArgs* a) {
+    const uint32_t per = a->ident ? a->wstride : a->wstride + a->rstride;
+    uint32_t R = std::max<uint32_t>(16, (kAosTileBytes / per) & ~15u);
+    a->R = R;
+    const uint32_t wimg = (R * a->wstride + 15) & ~15u;
+    a->simg = a->ident ? 0 : wimg;
+    const uint32_t end = a->ident ? wimg : wimg + ((R * a->rstride + 15) & ~15u);
+    return end + (a->prefix_len ? 2 * a->L : 0);
+}
+
 __global__ void k_aos_status(srpc_unpack_status* st, uint32_t flags, uint64_t first_bad) {
     if (threadIdx.x == 0) {
         st->flags = flags;
@@ -164,8 +308,23 @@ int aos_args(const srpc_plan* p, const void* recs, uint64_t stride, const uint32
     a->rstride = static_cast<uint32_t>(stride);
     a->prefix_len = p->prefix_len;
     a->L = p->tile_L;
+    a->ident = p->prefix_len == 0 && stride == p->stride;
+    uint64_t covered = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        a->ident = a->ident && offs[f] == p->off[f];
+        covered += p->size[f];
+    }
+    // fields do not overlap (each has its own bytes in a C++ struct), so they
+    // cover the struct when their sizes add up to its stride
+    a->cover = covered == stride;
     return SRPC_OK;
 }
+
+// A/B switch (SRPC_AOS_UNSTAGED=1 in the environment at load): the per-field kernels only.
+const bool g_aos_unstaged = [] {
+    const char* e = std::getenv("SRPC_AOS_UNSTAGED");
+    return e && e[0] == '1';
+}();
 
 }  // namespace
 }  // namespace srpc_impl
@@ -183,6 +342,14 @@ int srpc_gpu_pack_aos(const srpc_plan* p, const void* d_records, uint64_t record
     if (!d_records || !d_wire) return SRPC_E_INVALID;
     if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
     if (!aligned(d_wire, 16)) return SRPC_E_ALIGN;
+    if (aligned(d_records, 16) && !g_aos_unstaged) {
+        const uint32_t lds = staged_tiling(&a);
+        const uint64_t tiles = (n + a.R - 1) / a.R;
+        if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_pack_aos_staged, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), lds, static_cast<hipStream_t>(stream),
+               a, static_cast<const uint8_t*>(d_records), d_wire, n, lds - (a.prefix_len ? 2 * a.L : 0));
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
     a.R = p->ptile_R;
     const uint64_t tiles = (n + a.R - 1) / a.R;
     if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
@@ -210,7 +377,13 @@ int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire
     } else {
         n_fit = n;
     }
-    if (n_fit) {
+    if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
+        const uint32_t lds = staged_tiling(&a);
+        const uint64_t tiles = (n_fit + a.R - 1) / a.R;
+        if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_unpack_aos_staged, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), lds, s, a, d_wire,
+               static_cast<uint8_t*>(d_records), n_fit, d_status, lds - (a.prefix_len ? 2 * a.L : 0));
+    } else if (n_fit) {
         a.R = p->tile_R;
         const uint64_t tiles = (n_fit + a.R - 1) / a.R;
         if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;

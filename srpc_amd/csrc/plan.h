@@ -217,6 +217,7 @@ struct srpc_plan {
         int k = 0, kw = 0;           // column chunks / wire chunks per lane
     } wtp, wtu;                      // pack, unpack
     bool all4 = false;              // every field 4 bytes (DWORD x4 variant eligible)
+    int rec_id = -1;                 // TILE: schema-specialised kernels (rec.hip), -1 none
     srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
     // string schemas (SRPC_PATH_VAR)
     uint32_t nstrings = 0;

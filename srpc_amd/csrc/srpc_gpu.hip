@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "plan.h"
+#include "rec.h"
 #include "srpc_gpu.h"
 
 namespace {
@@ -61,6 +62,7 @@ struct TileArgs {
     uint32_t prefix_len;
     uint32_t R;                      // records per tile (multiple of 16)
     uint32_t L;                      // template period lcm(stride, 16), divides R*stride
+    uint64_t base;                   // unpack: index of the wire's first record (status reports)
 };
 
 
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(kWave) void k_unpack_tile_wave(TileArgs a, const ui
                 const uint32_t wd = d0 ? 0 : d1 ? 1 : d2 ? 2 : 3;
                 const uint32_t dw = d0 ? d0 : d1 ? d1 : d2 ? d2 : d3;
                 const uint32_t i = 16 * c + 4 * wd + (__builtin_ctz(dw) >> 3);
-                report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                report_bad(st, SRPC_STATUS_PREFIX, a.base + rbase + i / a.stride);
             }
         }
         *reinterpret_cast<uint4*>(img + 16 * c) = v;
@@ -627,7 +629,7 @@ __global__ __launch_bounds__(kWave) void k_unpack_tile_wave(TileArgs a, const ui
         for (uint32_t i = full * 16; i < tbytes; ++i) {
             const uint8_t b = src[i];
             const uint32_t ph = i % a.L;
-            if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph]) report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+            if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph]) report_bad(st, SRPC_STATUS_PREFIX, a.base + rbase + i / a.stride);
             img[i] = b;
         }
     }
@@ -701,7 +703,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
                         const uint32_t w = d0 ? 0 : d1 ? 1 : d2 ? 2 : 3;
                         const uint32_t dw = d0 ? d0 : d1 ? d1 : d2 ? d2 : d3;
                         const uint32_t i = 16 * c + 4 * w + (__builtin_ctz(dw) >> 3);
-                        report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                        report_bad(st, SRPC_STATUS_PREFIX, a.base + rbase + i / a.stride);
                     }
                 }
                 *reinterpret_cast<uint4*>(img + 16 * c) = v;
@@ -712,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
                 const uint8_t b = src[i];
                 const uint32_t ph = i % a.L;
                 if (a.prefix_len && st && (b & mask[ph]) != tmpl[ph])
-                    report_bad(st, SRPC_STATUS_PREFIX, rbase + i / a.stride);
+                    report_bad(st, SRPC_STATUS_PREFIX, a.base + rbase + i / a.stride);
                 img[i] = b;
             }
         }
@@ -1165,6 +1167,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             (void)srpc_plan_destroy(p);
             return SRPC_E_HIP;
         }
+        if (p->path == SRPC_PATH_TILE) p->rec_id = rec_kernel_for(p);
     }
     *out = p;
     return SRPC_OK;
@@ -1204,6 +1207,7 @@ int srpc_plan_force_path(srpc_plan* p, int path) {
     }
     if (path == SRPC_PATH_TILE && p->tile_R) {
         p->path = path;
+        p->rec_id = rec_kernel_for(p);
         return SRPC_OK;
     }
     return SRPC_E_UNSUPPORTED;
@@ -1252,6 +1256,10 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
     case SRPC_TUNE_WAVE_UNPACK_BYTES:
         if (value < 0 || value > 65536 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         return configure_wave_tile(p, p->wtu, static_cast<uint32_t>(value));
+    case SRPC_TUNE_REC_KERNEL:
+        if (value < 0 || value > 1 || p->has_string) return SRPC_E_INVALID;
+        p->rec_id = value && p->path == SRPC_PATH_TILE ? rec_kernel_for(p) : -1;
+        return SRPC_OK;
     case SRPC_TUNE_PACK_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         configure_pack_tile(p, static_cast<uint32_t>(value));
@@ -1277,6 +1285,21 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
         DwordVariant v = p->dv;
         v.rpl = x4 ? 4 : 1;
         return launch_dword_any(true, m, wire, n, static_cast<uint32_t>(p->stride / 4), v, s);
+    }
+    // schema-specialised kernels (rec.hip) for the whole tiles, the generic
+    // ones for the rest
+    const void* rest[kMaxFields];
+    if (p->rec_id >= 0 && check_cols_aligned(cols, p->nfields, 16)) {
+        const uint64_t TR = rec_tile_records(p->rec_id), tiles = n / TR;
+        if (tiles) {
+            if (int rc2 = rec_pack(p->rec_id, p, cols, tiles, wire, s)) return rc2;
+            const uint64_t done = tiles * TR;
+            if (done == n) return SRPC_OK;
+            for (uint32_t f = 0; f < p->nfields; ++f) rest[f] = static_cast<const uint8_t*>(cols[f]) + done * p->size[f];
+            cols = rest;
+            n -= done;
+            wire += done * p->stride;
+        }
     }
     if (p->wtp.R && n / p->wtp.R < (1ull << 26)) {
         TileArgs a = make_tile_args(p, cols, true);
@@ -1340,6 +1363,21 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         n_fit = n;
     }
     if (n_fit == 0) return ret;
+    void* rest[kMaxFields];
+    uint64_t base = 0;  // records before `wire` (status reports of the generic kernels)
+    if (p->path == SRPC_PATH_TILE && p->rec_id >= 0 &&
+        check_cols_aligned(reinterpret_cast<const void* const*>(cols), p->nfields, 16)) {
+        const uint64_t TR = rec_tile_records(p->rec_id), tiles = n_fit / TR;
+        if (tiles) {
+            if (int rc2 = rec_unpack(p->rec_id, p, wire, tiles, cols, st, s)) return rc2;
+            base = tiles * TR;
+            if (base == n_fit) return ret;
+            for (uint32_t f = 0; f < p->nfields; ++f) rest[f] = static_cast<uint8_t*>(cols[f]) + base * p->size[f];
+            cols = rest;
+            n_fit -= base;
+            wire += base * p->stride;
+        }
+    }
     if (p->path == SRPC_PATH_DWORD) {
         const DwordMap m = make_dword_map(p, reinterpret_cast<const void* const*>(cols));
         const bool x4 = p->dv.rpl == 4 && p->all4 &&
@@ -1353,6 +1391,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     if (p->wtu.R && n_fit / p->wtu.R < (1ull << 26)) {
         TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
         a.R = p->wtu.R;
+        a.base = base;
         const uint32_t grid = static_cast<uint32_t>((n_fit + a.R - 1) / a.R);
         const size_t lds = p->wtu.lds;
 #define SRPC_UW(K, KW) launch(k_unpack_tile_wave<K, KW>, dim3(grid), dim3(kWave), lds, s, a, wire, n_fit, st)
@@ -1377,7 +1416,8 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
         return ret;
     }
     const uint64_t ntiles = (n_fit + p->tile_R - 1) / p->tile_R;
-    const TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
+    TileArgs a = make_tile_args(p, reinterpret_cast<const void* const*>(cols), false);
+    a.base = base;
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, p->tile_full_grid ? (1u << 30) : p->tile_grid));
     launch(k_unpack_tile, dim3(grid), dim3(kBlock), p->tile_lds, s, a, wire, n_fit, ntiles, st);
     if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;

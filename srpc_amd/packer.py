@@ -135,13 +135,15 @@ class GpuPacker:
              grid: int | None = None, pack_tile_bytes: int | None = None,
              var_kernel: int | None = None, var_image_bytes: int | None = None,
              var_chars_bytes: int | None = None, wave_pack_bytes: int | None = None,
-             wave_unpack_bytes: int | None = None) -> None:
+             wave_unpack_bytes: int | None = None, rec_kernel: int | None = None) -> None:
         """Performance knobs (srpc_plan_tune); output bytes never change.
-        var_kernel: VAR pack, 1 = record tiles (one pass), 0 = scan + chunk walk."""
+        var_kernel: VAR pack, 1 = record tiles (one pass), 0 = scan + chunk walk.
+        rec_kernel: TILE, 1 = schema-specialised kernels where the layout has one."""
         L = _lib.lib()
         for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal), (4, tile_bytes),
                           (5, grid), (9, pack_tile_bytes), (7, var_kernel), (8, var_image_bytes),
-                          (10, var_chars_bytes), (11, wave_pack_bytes), (12, wave_unpack_bytes)):
+                          (10, var_chars_bytes), (11, wave_pack_bytes), (12, wave_unpack_bytes),
+                          (13, rec_kernel)):
             if val is not None:
                 check(L.srpc_plan_tune(self._h, knob, int(val)), "srpc_plan_tune")
 

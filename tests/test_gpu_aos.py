@@ -53,9 +53,15 @@ def layout(recs, nfields):
 
 
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 1000, 4099, 100_003])
-@pytest.mark.parametrize("schema,envelope", [("quad", None), ("all", None), ("all", "request"), ("number", "response"),
-                                             ("i64_i8", None), ("wide", "request")])
-def test_aos_pack_unpack_vs_oracle(n, schema, envelope):
+@pytest.mark.parametrize("schema,envelope,vptr,shift", [
+    ("quad", None, True, 0), ("all", None, True, 0), ("all", "request", True, 0), ("number", "response", True, 0),
+    ("i64_i8", None, True, 0), ("wide", "request", True, 0),
+    # no vtable slot: Quad's struct is its wire body (the tile-copy kernels);
+    # Number's fields cover the struct (no read-back of the struct tile)
+    ("quad", None, False, 0), ("number", "response", False, 0), ("all", "request", False, 0),
+    # a struct array 8 bytes off 16-byte alignment: the per-field kernels
+    ("quad", None, True, 8), ("all", "request", True, 8)])
+def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
     kinds = {"quad": [oracle.INT32] * 4,
              "all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
              "number": [oracle.INT32], "i64_i8": [oracle.INT64, oracle.INT8],
@@ -64,27 +70,34 @@ def test_aos_pack_unpack_vs_oracle(n, schema, envelope):
     p = (GpuPacker.for_request(sch, "Svc_servicer::m") if envelope == "request"
          else GpuPacker.for_response(sch, 0) if envelope == "response" else GpuPacker(sch))
     rng = np.random.default_rng(n + len(kinds))
-    recs = random_records(kinds, n, rng)
+    recs = random_records(kinds, n, rng, vptr)
     stride, offs = layout(recs, len(kinds))
     cols = [np.ascontiguousarray(recs[f"f{i}"]) for i in range(len(kinds))]
     want = bytes(oracle.pack(kinds, cols, n, p.prefix))
-    d_recs = dev(recs.view(np.uint8))
+
+    def on_dev(a):  # the struct bytes at `shift` bytes into a 16-byte aligned allocation
+        t = empty(a.nbytes + 32)
+        t[shift:shift + a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1).copy()))
+        return t[shift:]
+
+    d_recs = on_dev(recs)
     wire = empty(p.wire_bytes(n) + 16)
     p.pack_aos(d_recs, stride, offs, n, wire)
     assert host(wire, p.wire_bytes(n)).tobytes() == want
     # unpack into a device copy of different structs: only the leaf bytes change
-    other = random_records(kinds, n, np.random.default_rng(7 + n), True)
-    d_other = dev(other.view(np.uint8))
+    other = random_records(kinds, n, np.random.default_rng(7 + n), vptr)
+    d_other = on_dev(other)
     st = status_buf()
     assert p.unpack_aos(dev(np.frombuffer(want, np.uint8)), len(want), n, d_other, stride, offs, st) == 0
     assert read_status(st) == (0, 2**64 - 1)
     back = host(d_other, n * stride).view(recs.dtype)
     for i in range(len(kinds)):
         assert back[f"f{i}"].tobytes() == recs[f"f{i}"].tobytes(), i
-    assert back["_vptr"].tobytes() == other["_vptr"].tobytes()
+    if vptr:
+        assert back["_vptr"].tobytes() == other["_vptr"].tobytes()
     # padding bytes are those of `other`
     mask = np.zeros(stride, bool)
-    mask[0:8] = True
+    mask[0:8 if vptr else 0] = True
     for o, k in zip(offs, kinds):
         mask[o:o + oracle.KIND_SIZE[k]] = True
     pad = np.flatnonzero(~mask)

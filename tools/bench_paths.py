@@ -95,16 +95,17 @@ def main():
                      "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
                      "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
 
-    def aos_case(name, sch, n):
+    def aos_case(name, sch, n, vptr=True):
         """Records as C-aligned structs behind an 8-byte vtable slot (a C++
-        std::vector<T> copied to the device): srpc_gpu_pack_aos / unpack_aos.
-        Algorithmic bytes: the whole struct array (read by pack, written by
-        unpack) + the wire."""
+        std::vector<T> of srpc messages copied to the device; vptr=False: a
+        plain struct): srpc_gpu_pack_aos / unpack_aos.  Algorithmic bytes: the
+        whole struct array (read by pack, written by unpack) + the wire."""
         if args.only not in name:
             return
         p = GpuPacker(sch)
-        fmts = [np.uint64] + [np.dtype(oracle.KIND_DTYPE[k]) for k in sch.kinds]
-        dt = np.dtype({"names": ["_v"] + [f"f{i}" for i in range(len(sch.kinds))], "formats": fmts}, align=True)
+        fmts = ([np.uint64] if vptr else []) + [np.dtype(oracle.KIND_DTYPE[k]) for k in sch.kinds]
+        dt = np.dtype({"names": (["_v"] if vptr else []) + [f"f{i}" for i in range(len(sch.kinds))], "formats": fmts},
+                      align=True)
         rng = np.random.default_rng(3)
         recs = rng.integers(0, 256, n * dt.itemsize, dtype=np.uint8).view(dt)
         for i, k in enumerate(sch.kinds):
@@ -206,6 +207,7 @@ def main():
     fixed_case("square_request_53B_16M", NUMBER, N, srpc_amd.request_prefix(SQUARE_METHOD, "Number"))
     fixed_case("square_response_19B_16M", NUMBER, N, srpc_amd.response_prefix(0, "Number"))
     aos_case("quad_aos_16M", QUAD, N)
+    aos_case("quad_aos_plain_16M", QUAD, N, vptr=False)
     aos_case("all_kinds_aos_16M", Schema.of("all_kinds", ("a", "bool"), ("b", "int8"), ("c", "char"),
                                             ("d", "int16"), ("e", "int32"), ("f", "int64")), N)
     var_case("multiple_primitives_str0-64_4M", [oracle.INT8, oracle.CHAR, oracle.INT64, oracle.STRING],
