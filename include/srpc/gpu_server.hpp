@@ -279,8 +279,9 @@ public:
         uint64_t walked = 0;   // bytes of whole frames found so far (frames _h_offs[0..nf))
         uint64_t nf = 0;
         bool eof = false;
+        bool buffered = false;  // whole frames already wait in _h_in: walk them before blocking in recv
         while (true) {
-            if (!eof) {
+            if (!eof && !buffered) {
                 // cap - have > 0 here: a full buffer is always consumed below,
                 // so recv returning 0 is the peer's orderly shutdown
                 auto t0 = clock::now();
@@ -290,6 +291,7 @@ public:
                 if (k <= 0) eof = true;
                 else have += static_cast<uint64_t>(k);
             }
+            buffered = false;
             // frame boundaries (the only per-frame CPU work on the fast path)
             uint64_t next_len = 0;
             bool next_hdr = false;
@@ -321,6 +323,11 @@ public:
                 if (!serve_oversize(fd, have, st)) return st;
                 have = 0;
             }
+            // A batch ends at max_batch frames, so the buffer can still hold
+            // whole frames (frames shorter than the method's fin) while the
+            // peer, having sent everything, waits for their answers: serve
+            // them before the next recv, which would block.
+            buffered = have >= 4 && have - 4 >= be32_at(_h_in);
         }
         return st;  // bytes of a cut final frame are dropped, as the reference's recv_data does
     }

@@ -855,6 +855,12 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     const uint64_t g = (C + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     const TimedCall timed;
+    if (g_force_single.load(std::memory_order_relaxed) == 2 && stream1_decodes(p)) {
+        // the single pass on its own (no chunk pipeline, no indexed decode)
+        void* s1 = base + r256(L.total);
+        if (int rc = stream1_launch(p, wire, wire_len, n, rec_offs, cols, str_offs, st, s1, nullptr, s)) return rc;
+        return wire_len ? stream1_note(p, wire_len, s1, st, nullptr, s) : SRPC_OK;
+    }
     const uint64_t nblk = (C + 255) / 256;
     auto* parts = reinterpret_cast<uint64_t*>(base + L.parts);
     launch(k_stream_ctl_reset, dim3(static_cast<uint32_t>(std::min<uint64_t>((nblk + 255) / 256 + 1, 1024))),
@@ -907,5 +913,5 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
 // runs the single-pass kernels whatever the chunk pipeline found, 0 = only
 // when it leaves chunks wrong.  Returns the previous setting.
 extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_force_single(int on) {
-    return static_cast<int>(srpc_impl::g_force_single.exchange(on ? 1u : 0u));
+    return static_cast<int>(srpc_impl::g_force_single.exchange(static_cast<uint32_t>(on < 0 ? 0 : on > 2 ? 2 : on)));
 }

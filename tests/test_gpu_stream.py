@@ -17,7 +17,7 @@ Tests taking the `path` fixture run twice: the chunk pipeline as it chooses
 ("auto": the single pass only when chunks stay wrong after the repair
 rounds), and with every stream handed to the single-pass decode ("single",
 the srpc_debug_stream_force_single test hook), so both decoders meet the
-same cases.
+same cases; "only" runs the single pass alone (no chunk pipeline before it).
 """
 import ctypes
 import json
@@ -41,11 +41,11 @@ from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty
 RES_ROUNDS, RES_SINGLE, RES_SINGLE_LEFT = 1, 2, 4  # srpc_unpack_status.reserved bits (srpc_gpu.h)
 
 
-@pytest.fixture(params=["auto", "single"])
+@pytest.fixture(params=["auto", "single", "only"])
 def path(request):
     hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
     hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
-    prev = hook(1 if request.param == "single" else 0)
+    prev = hook({"auto": 0, "single": 1, "only": 2}[request.param])
     yield request.param
     hook(prev)
 
@@ -148,9 +148,7 @@ def test_random_streams(n, schema, maxlen, envelope, path):
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
     r = stream_unpack.last_reserved
-    if path == "auto":  # random strings: the chunk pipeline settles, no hand-over
-        assert not r & RES_SINGLE, r
-    elif n:
+    if path != "auto" and n:
         # a single-pass block's entry is almost always one of its candidates
         # (blocks that waited for their predecessor's state: bits 8-31)
         blocks = (len(wire) + 8191) // 8192
@@ -185,8 +183,8 @@ def test_zero_heavy_streams_misspeculate_and_fix(n, path):
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
     r = stream_unpack.last_reserved
-    assert r & RES_ROUNDS, "expected chains that leave the speculation on zero-heavy data"
-    assert (path == "single") <= bool(r & RES_SINGLE)
+    assert path == "only" or r & RES_ROUNDS, "expected chains that leave the speculation on zero-heavy data"
+    assert (path != "auto") <= bool(r & RES_SINGLE)
 
 
 def _error_case(p, kinds, wire, n):

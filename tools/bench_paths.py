@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--var-kernel", default="", help="VAR cases: comma list of pack kernels to time "
                     "(1 record tiles, 0 scan + walk; default: the plan's default)")
     ap.add_argument("--var-caps", default="", help="VAR record tiles: IMAGE:CHARS bytes (default: the plan's)")
+    ap.add_argument("--rec-ab", action="store_true",
+                    help="fixed cases: also time the generic TILE kernels (rec_kernel=0) beside the default")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="VAR cases: skip the index-free stream decode timing")
     args = ap.parse_args()
@@ -89,11 +91,18 @@ def main():
         tp = timeit(lambda: p.pack(dcols, n, wire, stream=s))
         tu = timeit(lambda: p.unpack(wire, n * p.record_bytes, n, back, stream=s))
         ok = ok and all(torch.equal(a, b) for a, b in zip(dcols, back))
+        generic = {}
+        if args.rec_ab and p.path == 2:
+            p.tune(rec_kernel=0)
+            gp = timeit(lambda: p.pack(dcols, n, wire, stream=s))
+            gu = timeit(lambda: p.unpack(wire, n * p.record_bytes, n, back, stream=s))
+            p.tune(rec_kernel=1)
+            generic = {"generic_pack_frac": round(alg / gp / 8e12, 4), "generic_unpack_frac": round(alg / gu / 8e12, 4)}
         rows.append({"case": name, "path": {1: "dword", 2: "tile", 3: "var"}[p.path], "records": n,
                      "record_bytes": p.record_bytes, "alg_bytes": alg, "pack_us": round(tp * 1e6, 2),
                      "unpack_us": round(tu * 1e6, 2), "pack_GBps": round(alg / tp / 1e9, 1),
                      "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
-                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
+                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok), **generic})
 
     def aos_case(name, sch, n, vptr=True):
         """Records as C-aligned structs behind an 8-byte vtable slot (a C++
@@ -224,6 +233,8 @@ def main():
             f.write(txt)
     for r in rows:
         extra = f'  stream {r["stream_us"]:8.1f} us ({r["stream_frac"]:.3f})' if "stream_us" in r else ""
+        if "generic_pack_frac" in r:
+            extra += f'  generic ({r["generic_pack_frac"]:.3f} / {r["generic_unpack_frac"]:.3f})'
         print(f'{r["case"]:34s} {r["path"]:5s} pack {r["pack_us"]:9.1f} us {r["pack_GBps"]:7.1f} GB/s '
               f'({r["pack_frac"]:.3f})  unpack {r["unpack_us"]:9.1f} us {r["unpack_GBps"]:7.1f} GB/s '
               f'({r["unpack_frac"]:.3f})  parity={r["parity_ok"]}{extra}')

@@ -68,7 +68,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--single", action="store_true", help="hand every stream to the single-pass decode")
+    ap.add_argument("--single", type=int, default=0,
+                    help="1: hand every stream to the single-pass decode after the chunk pipeline; "
+                         "2: the single pass alone")
     args = ap.parse_args()
 
     import numpy as np
@@ -82,7 +84,7 @@ def main():
         import ctypes
         hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
         hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
-        hook(1)
+        hook(args.single)
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream()
     rows = []
