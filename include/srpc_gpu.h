@@ -150,8 +150,10 @@ int srpc_plan_force_path(srpc_plan* plan, int path);
                                         multiple of 16); larger tiles take the walk  */
 #define SRPC_TUNE_VAR_CHARS_BYTES 10 /* VAR record tiles: LDS chars stage bytes
                                         (0..65536, multiple of 16)                   */
-#define SRPC_TUNE_REC_KERNEL 13      /* TILE path: 1 = schema-specialised kernels for the
-                                        layouts that have one (default), 0 = generic */
+#define SRPC_TUNE_REC_KERNEL 13      /* TILE path: schema-specialised kernels for the
+                                        layouts that have one: 1 = in the directions
+                                        where they measured faster (default), 2 = both
+                                        directions, 0 = generic kernels only        */
 #define SRPC_TUNE_GRID 5             /* DWORD path: max workgroups (0 = one per
                                         256*iter records; else grid-stride)       */
 int srpc_plan_tune(srpc_plan* plan, int knob, int value);

@@ -23,7 +23,9 @@
 // the struct (padding, a vtable pointer) the struct tile is read first so
 // those bytes are written back unchanged.  When the struct's layout is the
 // wire body's (same offsets and stride, no prefix -- e.g. Quad) the two images
-// are one and the kernels are tile copies.  A struct array that is only
+// are one and the kernels are tile copies.  When the fields are one run of the
+// struct (Quad behind a vtable pointer), one lane moves each record's run
+// straight between HBM arrays (k_pack_aos_run).  A struct array that is only
 // naturally aligned takes the per-field kernels (one struct per lane, fields
 // straight between HBM and the wire image).
 #include <hip/hip_runtime.h>
@@ -47,6 +49,7 @@ struct AosArgs {
     uint32_t simg;              // staged kernels: LDS offset of the struct image (0: the wire image's, ident)
     bool ident;                 // struct layout == wire layout
     bool cover;                 // the leaf fields cover every byte of the struct
+    int32_t boff;               // >= 0: the wire body is struct bytes [boff, boff + wstride) (no prefix)
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -151,6 +154,64 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos(AosArgs a, const uint8_t*
         const uint32_t s = e * a.wstride;
         for (uint32_t f = 0; f < a.nfields; ++f) store_field(dst + a.roff[f], lds_u64(lds, s + a.woff[f]), a.size[f]);
     }
+}
+
+// A struct whose leaf fields sit back to back in wire order (Quad behind a
+// vtable pointer: bytes 8..23 of 24) and no prefix: each record is one run of
+// W bytes, moved between the struct array and the wire in 8-byte pieces
+// straight from HBM to HBM, one record per lane (no LDS: the wire side is
+// contiguous, the struct side is strided runs the L2 merges into lines).
+template <uint32_t W>
+__global__ __launch_bounds__(kBlock) void k_pack_aos_run(const uint8_t* __restrict__ recs, uint32_t rstride,
+                                                         uint32_t boff, uint8_t* __restrict__ wire, uint64_t n) {
+    const uint64_t e = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(recs + e * rstride + boff);
+    uint64_t* d = reinterpret_cast<uint64_t*>(wire + e * W);
+    uint64_t v[W / 8];
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) v[k] = __builtin_nontemporal_load(s + k);
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) __builtin_nontemporal_store(v[k], d + k);
+}
+
+template <uint32_t W>
+__global__ __launch_bounds__(kBlock) void k_unpack_aos_run(const uint8_t* __restrict__ wire, uint8_t* __restrict__ recs,
+                                                           uint32_t rstride, uint32_t boff, uint64_t n) {
+    const uint64_t e = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(wire + e * W);
+    uint64_t* d = reinterpret_cast<uint64_t*>(recs + e * rstride + boff);
+    uint64_t v[W / 8];
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) v[k] = __builtin_nontemporal_load(s + k);
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) __builtin_nontemporal_store(v[k], d + k);
+}
+
+// The run kernels for wire bodies of 8, 16, 24 or 32 bytes (8-byte aligned
+// struct array, stride and body offset), else false.
+bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+    if (a.boff < 0 || (a.wstride != 8 && a.wstride != 16 && a.wstride != 24 && a.wstride != 32) || a.rstride % 8 ||
+        a.boff % 8 || !aligned(src, 8) || !aligned(dst, 8))
+        return false;
+    const uint64_t g = (n + kBlock - 1) / kBlock;
+    if (g > 0x7fffffffull) return false;
+    const uint32_t boff = static_cast<uint32_t>(a.boff);
+#define SRPC_AOS_RUN(Wb)                                                                                         \
+    if (a.wstride == Wb) {                                                                                       \
+        if (pack) launch(k_pack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, a.rstride, \
+                         boff, dst, n);                                                                          \
+        else launch(k_unpack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, dst,         \
+                    a.rstride, boff, n);                                                                         \
+        return true;                                                                                             \
+    }
+    SRPC_AOS_RUN(8)
+    SRPC_AOS_RUN(16)
+    SRPC_AOS_RUN(24)
+    SRPC_AOS_RUN(32)
+#undef SRPC_AOS_RUN
+    return false;
 }
 
 // HBM bytes [0, bytes) of a tile -> LDS (16-byte pieces, then single bytes).
@@ -317,6 +378,14 @@ int aos_args(const srpc_plan* p, const void* recs, uint64_t stride, const uint32
     // fields do not overlap (each has its own bytes in a C++ struct), so they
     // cover the struct when their sizes add up to its stride
     a->cover = covered == stride;
+    // the body as one run of the struct: every field at the same shift from its wire offset
+    a->boff = -1;
+    if (p->prefix_len == 0 && p->nfields && offs[0] >= p->off[0]) {
+        const uint32_t sh = offs[0] - p->off[0];
+        bool run = sh + p->stride <= stride;
+        for (uint32_t f = 0; f < p->nfields; ++f) run = run && offs[f] == p->off[f] + sh;
+        if (run) a->boff = static_cast<int32_t>(sh);
+    }
     return SRPC_OK;
 }
 
@@ -342,6 +411,9 @@ int srpc_gpu_pack_aos(const srpc_plan* p, const void* d_records, uint64_t record
     if (!d_records || !d_wire) return SRPC_E_INVALID;
     if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
     if (!aligned(d_wire, 16)) return SRPC_E_ALIGN;
+    if (!a.ident && !g_aos_unstaged &&
+        launch_aos_run(a, true, static_cast<const uint8_t*>(d_records), d_wire, n, static_cast<hipStream_t>(stream)))
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (aligned(d_records, 16) && !g_aos_unstaged) {
         const uint32_t lds = staged_tiling(&a);
         const uint64_t tiles = (n + a.R - 1) / a.R;
@@ -377,6 +449,9 @@ int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire
     } else {
         n_fit = n;
     }
+    if (n_fit && !a.ident && !g_aos_unstaged &&
+        launch_aos_run(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
+        return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
     if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
         const uint32_t lds = staged_tiling(&a);
         const uint64_t tiles = (n_fit + a.R - 1) / a.R;

@@ -218,6 +218,7 @@ struct srpc_plan {
     } wtp, wtu;                      // pack, unpack
     bool all4 = false;              // every field 4 bytes (DWORD x4 variant eligible)
     int rec_id = -1;                 // TILE: schema-specialised kernels (rec.hip), -1 none
+    bool rec_pack = false, rec_unpack = false;  // ... used for pack / unpack
     srpc_impl::DwordVariant dv;      // DWORD-path variant (srpc_plan_tune)
     // string schemas (SRPC_PATH_VAR)
     uint32_t nstrings = 0;

@@ -13,6 +13,9 @@ namespace srpc_impl {
 
 // The instance for the plan's layout (prefix length and field sizes), or -1.
 int rec_kernel_for(const srpc_plan* p);
+// Whether instance `id`'s pack / unpack kernel beat the generic TILE kernels
+// (tools/bench_paths.py --rec-ab, profiles/r03_paths_rec_ab.log).
+bool rec_default(int id, bool pack);
 // Records per tile of instance `id` (its kernels cover whole tiles only).
 uint64_t rec_tile_records(int id);
 // The first tiles * rec_tile_records(id) records; columns 16-byte aligned.

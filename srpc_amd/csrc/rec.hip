@@ -275,6 +275,7 @@ __global__ __launch_bounds__(kRecWave) void k_unpack_rec(RecArgs a, const uint8_
 
 // ---- instances ---------------------------------------------------------------
 struct RecKernel {
+    bool use_pack, use_unpack;  // measured faster than the generic kernels (rec_default)
     int prefix_len;
     int nf;
     int size[8];
@@ -285,8 +286,8 @@ struct RecKernel {
 };
 
 template <class L, int G, int K>
-constexpr RecKernel make_rec() {
-    RecKernel r{L::off(0), L::NF, {}, kRecWave * G * K, static_cast<size_t>(kRecWave) * G * K * L::STRIDE,
+constexpr RecKernel make_rec(bool use_pack, bool use_unpack) {
+    RecKernel r{use_pack, use_unpack, L::off(0), L::NF, {}, kRecWave * G * K, static_cast<size_t>(kRecWave) * G * K * L::STRIDE,
                 k_pack_rec<L, G, K>, k_unpack_rec<L, G, K>};
     for (int f = 0; f < L::NF; ++f) r.size[f] = L::SZ[f];
     return r;
@@ -298,12 +299,14 @@ constexpr RecKernel make_rec() {
 // multiply requests (55) and a response (19).  A layout matches by prefix
 // length and field sizes, whatever the prefix bytes.
 const RecKernel kRec[] = {
-    make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(),
-    make_rec<Lay<49, 4>, 4, 2>(),
-    make_rec<Lay<15, 4>, 4, 4>(),
-    make_rec<Lay<50, 4, 4>, 4, 2>(),
-    make_rec<Lay<55, 4, 4>, 4, 2>(),
-    make_rec<Lay<19, 4, 4>, 4, 4>(),
+    // (pack, unpack): where each measured faster than the generic TILE kernels
+    // (profiles/r03_paths_rec_ab.log; differences under ~0.02 of peak are noise)
+    make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(true, true),   // 0.64 / 0.68 -> 0.80 / 0.72
+    make_rec<Lay<49, 4>, 4, 2>(false, false),
+    make_rec<Lay<15, 4>, 4, 4>(false, false),
+    make_rec<Lay<50, 4, 4>, 4, 2>(false, true),
+    make_rec<Lay<55, 4, 4>, 4, 2>(false, false),
+    make_rec<Lay<19, 4, 4>, 4, 4>(false, true),
 };
 constexpr int kNumRec = sizeof(kRec) / sizeof(kRec[0]);
 
@@ -319,6 +322,10 @@ int rec_kernel_for(const srpc_plan* p) {
         if (same) return i;
     }
     return -1;
+}
+
+bool rec_default(int id, bool pack) {
+    return id >= 0 && id < kNumRec && (pack ? kRec[id].use_pack : kRec[id].use_unpack);
 }
 
 uint64_t rec_tile_records(int id) { return id >= 0 && id < kNumRec ? static_cast<uint64_t>(kRec[id].tile_records) : 0; }

@@ -1061,6 +1061,14 @@ int upload_prefix(srpc_plan* p) {
     return SRPC_OK;
 }
 
+// Schema-specialised kernels (rec.hip): mode 1 = in the directions where the
+// instance measured faster, 2 = both, 0 = none.
+void set_rec(srpc_plan* p, int mode) {
+    p->rec_id = mode ? rec_kernel_for(p) : -1;
+    p->rec_pack = p->rec_id >= 0 && (mode == 2 || rec_default(p->rec_id, true));
+    p->rec_unpack = p->rec_id >= 0 && (mode == 2 || rec_default(p->rec_id, false));
+}
+
 }  // namespace
 
 extern "C" {
@@ -1167,7 +1175,7 @@ int srpc_plan_create(const srpc_schema_desc* d, int device, srpc_plan** out) {
             (void)srpc_plan_destroy(p);
             return SRPC_E_HIP;
         }
-        if (p->path == SRPC_PATH_TILE) p->rec_id = rec_kernel_for(p);
+        if (p->path == SRPC_PATH_TILE) set_rec(p, 1);
     }
     *out = p;
     return SRPC_OK;
@@ -1207,7 +1215,7 @@ int srpc_plan_force_path(srpc_plan* p, int path) {
     }
     if (path == SRPC_PATH_TILE && p->tile_R) {
         p->path = path;
-        p->rec_id = rec_kernel_for(p);
+        set_rec(p, 1);
         return SRPC_OK;
     }
     return SRPC_E_UNSUPPORTED;
@@ -1257,8 +1265,8 @@ int srpc_plan_tune(srpc_plan* p, int knob, int value) {
         if (value < 0 || value > 65536 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
         return configure_wave_tile(p, p->wtu, static_cast<uint32_t>(value));
     case SRPC_TUNE_REC_KERNEL:
-        if (value < 0 || value > 1 || p->has_string) return SRPC_E_INVALID;
-        p->rec_id = value && p->path == SRPC_PATH_TILE ? rec_kernel_for(p) : -1;
+        if (value < 0 || value > 2 || p->has_string) return SRPC_E_INVALID;
+        set_rec(p, p->path == SRPC_PATH_TILE ? value : 0);
         return SRPC_OK;
     case SRPC_TUNE_PACK_TILE_BYTES:
         if (value < 1024 || value > 49152 || p->has_string || p->stride > kMaxTileStride) return SRPC_E_INVALID;
@@ -1289,7 +1297,7 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
     // schema-specialised kernels (rec.hip) for the whole tiles, the generic
     // ones for the rest
     const void* rest[kMaxFields];
-    if (p->rec_id >= 0 && check_cols_aligned(cols, p->nfields, 16)) {
+    if (p->rec_pack && check_cols_aligned(cols, p->nfields, 16)) {
         const uint64_t TR = rec_tile_records(p->rec_id), tiles = n / TR;
         if (tiles) {
             if (int rc2 = rec_pack(p->rec_id, p, cols, tiles, wire, s)) return rc2;
@@ -1365,7 +1373,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     if (n_fit == 0) return ret;
     void* rest[kMaxFields];
     uint64_t base = 0;  // records before `wire` (status reports of the generic kernels)
-    if (p->path == SRPC_PATH_TILE && p->rec_id >= 0 &&
+    if (p->path == SRPC_PATH_TILE && p->rec_unpack &&
         check_cols_aligned(reinterpret_cast<const void* const*>(cols), p->nfields, 16)) {
         const uint64_t TR = rec_tile_records(p->rec_id), tiles = n_fit / TR;
         if (tiles) {

@@ -138,7 +138,7 @@ class GpuPacker:
              wave_unpack_bytes: int | None = None, rec_kernel: int | None = None) -> None:
         """Performance knobs (srpc_plan_tune); output bytes never change.
         var_kernel: VAR pack, 1 = record tiles (one pass), 0 = scan + chunk walk.
-        rec_kernel: TILE, 1 = schema-specialised kernels where the layout has one."""
+        rec_kernel: TILE schema-specialised kernels, 1 = where measured faster, 2 = both directions, 0 = off."""
         L = _lib.lib()
         for knob, val in ((1, records_per_lane), (2, iters), (3, nontemporal), (4, tile_bytes),
                           (5, grid), (9, pack_tile_bytes), (7, var_kernel), (8, var_image_bytes),

@@ -13,11 +13,15 @@ orc_unpack) and the reference-produced fixtures:
   whose ends no block can guess (each such block waits for its predecessor);
 - streams cut short, foreign prefixes, fewer records than asked for, and
   trailing bytes after the n-th record.
-Tests taking the `path` fixture run twice: the chunk pipeline as it chooses
-("auto": the single pass only when chunks stay wrong after the repair
-rounds), and with every stream handed to the single-pass decode ("single",
-the srpc_debug_stream_force_single test hook), so both decoders meet the
-same cases; "only" runs the single pass alone (no chunk pipeline before it).
+Tests taking the `path` fixture run once per decoder (the
+srpc_debug_stream_force_single test hook): "auto" as the library chooses (the
+chunk pipeline + record index + indexed decode; when its chunks stay wrong,
+the speculative single pass of sdec.hip; when that gives up, the bounded one
+of stream1.hip); "handover" the same with the chunk pipeline's hand-over
+forced; "fast" the speculative pass alone, never giving up (every miss
+walked); "single" the speculative pass, then the bounded pass rewriting every
+output; "only" the bounded pass alone; "chunks" the chunk pipeline handing
+over to the bounded pass directly.  Every decoder meets the same cases.
 """
 import ctypes
 import json
@@ -41,11 +45,14 @@ from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty
 RES_ROUNDS, RES_SINGLE, RES_SINGLE_LEFT = 1, 2, 4  # srpc_unpack_status.reserved bits (srpc_gpu.h)
 
 
-@pytest.fixture(params=["auto", "single", "only"])
+MODES = {"auto": 0, "single": 1, "only": 2, "chunks": 3, "fast": 4, "handover": 6}
+
+
+@pytest.fixture(params=list(MODES))
 def path(request):
     hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
     hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
-    prev = hook({"auto": 0, "single": 1, "only": 2}[request.param])
+    prev = hook(MODES[request.param])
     yield request.param
     hook(prev)
 
@@ -148,7 +155,7 @@ def test_random_streams(n, schema, maxlen, envelope, path):
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n, len(p.prefix)))
     r = stream_unpack.last_reserved
-    if path != "auto" and n:
+    if path in ("single", "only") and n:
         # a single-pass block's entry is almost always one of its candidates
         # (blocks that waited for their predecessor's state: bits 8-31)
         blocks = (len(wire) + 8191) // 8192
@@ -183,8 +190,9 @@ def test_zero_heavy_streams_misspeculate_and_fix(n, path):
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, offs, n))
     r = stream_unpack.last_reserved
-    assert path == "only" or r & RES_ROUNDS, "expected chains that leave the speculation on zero-heavy data"
-    assert (path != "auto") <= bool(r & RES_SINGLE)
+    if path in ("chunks", "auto", "handover"):
+        assert r & RES_ROUNDS, "expected chains that leave the speculation on zero-heavy data"
+    assert (path in ("single", "only")) <= bool(r & RES_SINGLE)
 
 
 def _error_case(p, kinds, wire, n):

@@ -96,8 +96,12 @@ def main():
             p.tune(rec_kernel=0)
             gp = timeit(lambda: p.pack(dcols, n, wire, stream=s))
             gu = timeit(lambda: p.unpack(wire, n * p.record_bytes, n, back, stream=s))
+            p.tune(rec_kernel=2)
+            rp = timeit(lambda: p.pack(dcols, n, wire, stream=s))
+            ru = timeit(lambda: p.unpack(wire, n * p.record_bytes, n, back, stream=s))
             p.tune(rec_kernel=1)
-            generic = {"generic_pack_frac": round(alg / gp / 8e12, 4), "generic_unpack_frac": round(alg / gu / 8e12, 4)}
+            generic = {"generic_pack_frac": round(alg / gp / 8e12, 4), "generic_unpack_frac": round(alg / gu / 8e12, 4),
+                       "rec_pack_frac": round(alg / rp / 8e12, 4), "rec_unpack_frac": round(alg / ru / 8e12, 4)}
         rows.append({"case": name, "path": {1: "dword", 2: "tile", 3: "var"}[p.path], "records": n,
                      "record_bytes": p.record_bytes, "alg_bytes": alg, "pack_us": round(tp * 1e6, 2),
                      "unpack_us": round(tu * 1e6, 2), "pack_GBps": round(alg / tp / 1e9, 1),
@@ -215,6 +219,11 @@ def main():
                                               ("d", "int16"), ("e", "int32"), ("f", "int64")), N)
     fixed_case("square_request_53B_16M", NUMBER, N, srpc_amd.request_prefix(SQUARE_METHOD, "Number"))
     fixed_case("square_response_19B_16M", NUMBER, N, srpc_amd.response_prefix(0, "Number"))
+    two = Schema.of("TwoNumbers", ("left", "int32"), ("right", "int32"))
+    fixed_case("add_request_58B_16M", two, N, srpc_amd.request_prefix("Calculator_servicer::add", "TwoNumbers"))
+    fixed_case("subtract_request_63B_16M", two, N,
+               srpc_amd.request_prefix("Calculator_servicer::subtract", "TwoNumbers"))
+    fixed_case("two_numbers_response_23B_16M", two, N, srpc_amd.response_prefix(0, "TwoNumbers"))
     aos_case("quad_aos_16M", QUAD, N)
     aos_case("quad_aos_plain_16M", QUAD, N, vptr=False)
     aos_case("all_kinds_aos_16M", Schema.of("all_kinds", ("a", "bool"), ("b", "int8"), ("c", "char"),
@@ -234,7 +243,8 @@ def main():
     for r in rows:
         extra = f'  stream {r["stream_us"]:8.1f} us ({r["stream_frac"]:.3f})' if "stream_us" in r else ""
         if "generic_pack_frac" in r:
-            extra += f'  generic ({r["generic_pack_frac"]:.3f} / {r["generic_unpack_frac"]:.3f})'
+            extra += (f'  generic ({r["generic_pack_frac"]:.3f} / {r["generic_unpack_frac"]:.3f})'
+                      f'  rec ({r["rec_pack_frac"]:.3f} / {r["rec_unpack_frac"]:.3f})')
         print(f'{r["case"]:34s} {r["path"]:5s} pack {r["pack_us"]:9.1f} us {r["pack_GBps"]:7.1f} GB/s '
               f'({r["pack_frac"]:.3f})  unpack {r["unpack_us"]:9.1f} us {r["unpack_GBps"]:7.1f} GB/s '
               f'({r["unpack_frac"]:.3f})  parity={r["parity_ok"]}{extra}')

@@ -4,6 +4,7 @@
 # per-block limits: <= 8 SQ, <= 4 TCC counters).  Summarised per kernel into
 # gpurun_out/pmc_paths_<tag>.txt by tools/pmc_paths_table.py.
 # usage (through gpurun): bash tools/pmc_paths.sh <tag> <filter> [<filter> ...]
+# (PMC_TOOL=stream_bench.py PMC_ARGS='--single 2': the stream decode cases)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -11,7 +12,7 @@ TAG=$1
 shift
 for F in "$@"; do
   D=gpurun_out/pmc_${TAG}_$F
-  RUN="python3 tools/bench_paths.py --only $F --reps 3 $PMC_ARGS"
+  RUN="python3 tools/${PMC_TOOL:-bench_paths.py} --only $F --reps 3 $PMC_ARGS"
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/stats -o run --output-format csv -- $RUN > $D.stats.log 2>&1 || exit 1
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" \

@@ -69,8 +69,9 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default=None)
     ap.add_argument("--single", type=int, default=0,
-                    help="1: hand every stream to the single-pass decode after the chunk pipeline; "
-                         "2: the single pass alone")
+                    help="decoders (srpc_debug_stream_force_single, stream.hip): 0 default, 2 the bounded "
+                         "pass alone, 3 chunk pipeline -> bounded pass, 4 the speculative pass never giving "
+                         "up, 5 speculative pass -> bounded pass, 6 default with the hand-over forced")
     args = ap.parse_args()
 
     import numpy as np
@@ -154,10 +155,10 @@ def main():
         row = {"case": name, "records": n, "wire_bytes": W, "alg_bytes": alg, "us": round(t * 1e6, 2),
                "GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 8e12, 4), "parity_ok": bool(ok),
                "blocks": (W + 8191) // 8192, "missed_blocks": reserved >> 8, "diag_bits": reserved & 7,
-               "single_pass": bool(reserved & 2)}
+               "single_pass": bool(reserved & 2), "gave_up": bool(reserved & 8)}
         rows.append(row)
         print(f'{name:36s} {n:9d} rec {W / 2**20:8.1f} MiB  {row["us"]:9.1f} us  {row["GBps"]:7.1f} GB/s '
-              f'({row["frac"]:.3f})  parity={ok}  single={row["single_pass"]} missed {row["missed_blocks"]}/{row["blocks"]}',
+              f'({row["frac"]:.3f})  parity={ok}  bounded={row["single_pass"]} gave_up={row["gave_up"]} missed {row["missed_blocks"]}/{row["blocks"]}',
               flush=True)
 
     S, I8, C8, I16, I32, I64 = oracle.STRING, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64

@@ -19,12 +19,15 @@ sys.path.insert(0, ROOT)
 
 PHASES = ["stage", "speculate", "segments", "cand+AGG", "lookback(a)", "lookback(b)", "own+INC",
           "record walk+table", "fixed out", "chars out"]
+SD_PHASES = ["stage", "speculate+walk", "segments+scans", "AGG chain", "look-back", "own+INC", "table",
+             "fixed out", "chars out", "-"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sdec", action="store_true", help="the speculative decode (sdec.hip, -DSRPC_SDEC_PHASES)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +37,11 @@ def main():
     from srpc_amd import GpuPacker, Schema, _lib
     from tools.stream_bench import gen_random, gen_zero_heavy
 
-    fn = _lib.lib().srpc_debug_stream_phases
+    fn = _lib.lib().srpc_debug_sdec_phases if args.sdec else _lib.lib().srpc_debug_stream_phases
+    hook = _lib.lib().srpc_debug_stream_force_single
+    hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
+    hook(4 if args.sdec else 2)  # the speculative decode never giving up / the bounded pass alone
+    names = SD_PHASES if args.sdec else PHASES
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     dev = torch.device("cuda:0")
     S, I8, C8, I16, I32, I64 = oracle.STRING, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64
@@ -83,9 +90,13 @@ def main():
         life = tot / blocks / 2400
         print(f"  call {call_us:.1f} us; mean block lifetime {life:.1f} us -> {life * blocks / args.reps / call_us:.0f} "
               f"blocks resident on average")
-        for i, nm in enumerate(PHASES):
+        for i, nm in enumerate(names):
             cyc = h[i] / blocks
             print(f"  {nm:20s} {cyc:10.0f} cycles/block {cyc / 2400:8.2f} us  {100 * h[i] / max(tot, 1):5.1f} %")
+        if args.sdec:
+            print(f"  misses {h[12] / args.reps:.0f} per call; look-back depth {h[13] / blocks:.1f} blocks, "
+                  f"windows past the first {h[11] / blocks:.2f}, INC waits {h[14] / blocks:.3f} per block", flush=True)
+            continue
         print(f"  look-back: depth {h[13] / blocks:.1f} blocks, windows {h[11] / blocks:.2f}, "
               f"fast windows {h[14] / max(h[11], 1):.3f}, slow steps {h[12] / blocks:.2f} per block", flush=True)
 
