@@ -90,6 +90,7 @@ struct LaunchTimer {
     hipEvent_t stop = nullptr;
     bool armed = false;
     bool started = false;
+    int depth = 0;  // C-ABI calls in progress (one calls another: srpc_gpu_unpack_var_stream)
 };
 
 inline LaunchTimer& launch_timer() {
@@ -97,9 +98,14 @@ inline LaunchTimer& launch_timer() {
     return t;
 }
 
-// Disarms the timer when a C-ABI call returns (whatever it launched).
+// Disarms the timer when the outermost C-ABI call returns (whatever it and
+// the calls it made launched).
 struct TimedCall {
-    ~TimedCall() { launch_timer() = LaunchTimer{}; }
+    TimedCall() { ++launch_timer().depth; }
+    ~TimedCall() {
+        LaunchTimer& t = launch_timer();
+        if (--t.depth <= 0) t = LaunchTimer{};
+    }
 };
 
 // Launch a data-path kernel: the first launch of an armed call stamps

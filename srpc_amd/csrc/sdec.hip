@@ -117,6 +117,7 @@ struct SdArgs {
     const uint8_t* prefix;       // device copy (16 zero bytes past the end)
     uint64_t* rec_offs;
     uint64_t n, W;
+    uint64_t pre8, pre8_mask;    // the prefix's first (up to) 8 bytes, and which of them count
     uint32_t nfields, P, fixed_bytes;
     uint32_t fla;                // byte offset of the first string's length in a record
     uint32_t run[kMaxNS + 1];    // fixed bytes before string s (after the prefix), after the last
@@ -753,6 +754,11 @@ __global__ __launch_bounds__(kBlock) void k_sdec(SdArgs a, const uint8_t* __rest
                 const uint32_t j0 = __builtin_ctz(m);
                 uint32_t cl = (m >> j0) & 0xffu;  // candidates within 8 bytes of the first
                 m &= ~(0xffu << j0);
+                if (a.pre8_mask)  // an envelope: the prefix's first bytes, before any parse
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (((cl >> k) & 1) && ((rd.u64<true>(clo + j0 + k) ^ a.pre8) & a.pre8_mask))
+                            cl &= ~(1u << k);
                 uint64_t len[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
@@ -1324,9 +1330,16 @@ int sdec_launch(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint
     a.P = p->prefix_len;
     a.fixed_bytes = p->fixed_bytes;
     a.plaus = p->prefix_len >= 8 ? 1 : 2;
+    for (uint32_t i = 0; i < 8 && i < p->prefix_len; ++i) {
+        a.pre8 |= static_cast<uint64_t>(p->h_prefix[i]) << (8 * i);
+        a.pre8_mask |= 0xffull << (8 * i);
+    }
     a.nb = static_cast<uint32_t>(SL.nb);
     a.epoch = next_epoch();
-    a.miss_limit = miss_limit ? miss_limit : static_cast<uint32_t>(std::max<uint64_t>(32, SL.nb / 256));
+    // random data misses almost never (entry slots); data on which wrong
+    // starts parse misses in most blocks, each miss a wait on the look-back
+    // path: give up early
+    a.miss_limit = miss_limit ? miss_limit : static_cast<uint32_t>(8 + SL.nb / 4096);
     *abort_out = S.ctl + kCtlAbort;
     switch (p->nstrings) {
     case 1: launch_sdec<1>(a, wire, S, st, gate, s); break;

@@ -355,60 +355,6 @@ __device__ __forceinline__ void lds_window(const uint8_t* st, uint32_t o, uint32
 // a lane-0 walk was compute-bound, profiles/r02_stream_lds_ab.log.)
 constexpr uint32_t kStreamMargin = 2048;
 constexpr uint32_t kStreamStage = kBlock * kChunk + kStreamMargin + 32;
-// Candidate starts of a 64-byte chunk: bit j set when the four bytes at stage
-// offset o + j (o = the chunk's first byte + first_len_at + 4: the first string
-// length's high half) are zero -- a length read at a wrong offset almost never
-// has them, a true one (< 4 GiB) always.  o mod 16 is the same for every lane
-// of the workgroup (chunks are 64 bytes apart), so the 16-byte LDS reads and
-// the dword realignment are uniform; the test runs on byte-zero indicators
-// (0x80 per zero byte), four positions per dword.
-__device__ __forceinline__ uint64_t cand_mask64(const uint8_t* st, uint32_t o) {
-    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-    typedef const u32x4v __attribute__((address_space(3))) lds_u32x4c;
-    lds_u32x4c* q = reinterpret_cast<lds_u32x4c*>((lds_u8c*)st + (o & ~15u));
-    uint32_t w[24];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const u32x4v v = q[i];
-        w[4 * i] = v.x;
-        w[4 * i + 1] = v.y;
-        w[4 * i + 2] = v.z;
-        w[4 * i + 3] = v.w;
-    }
-    uint32_t d[17];
-    const uint32_t sh = o & 3;
-    switch (__builtin_amdgcn_readfirstlane((o >> 2) & 3)) {
-    case 0:
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-        break;
-    case 1:
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 2], w[k + 1], sh);
-        break;
-    case 2:
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 3], w[k + 2], sh);
-        break;
-    default:
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 4], w[k + 3], sh);
-        break;
-    }
-    uint32_t z[17];
-#pragma unroll
-    for (int k = 0; k < 17; ++k) z[k] = ~(((d[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d[k] | 0x7f7f7f7fu);
-    uint64_t m = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t a4 = z[k] & __builtin_amdgcn_alignbyte(z[k + 1], z[k], 1) &
-                            __builtin_amdgcn_alignbyte(z[k + 1], z[k], 2) &
-                            __builtin_amdgcn_alignbyte(z[k + 1], z[k], 3);
-        m |= static_cast<uint64_t>((((a4 >> 7) * 0x00204081u) >> 21) & 15u) << (4 * k);
-    }
-    return m;
-}
-
 __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const uint8_t* __restrict__ w, uint64_t W,
                                                           uint64_t C, Chunks ch) {
     __shared__ __attribute__((aligned(16))) uint8_t st[kStreamStage + 16];
@@ -439,19 +385,57 @@ __global__ __launch_bounds__(kBlock) void k_stream_chunks(StreamArgs a, const ui
     } else if (c == 0) {
         b = 0;  // the stream starts at 0: no speculation
     } else {
-        // the candidates at the chunk's 64 positions (cand_mask64), all lanes
-        // in step: a mask.  Then the candidates are parsed in order until one
-        // is plausible -- a lane parses only its few candidates, instead of
-        // the wave running the parse at every position some lane's filter
-        // passed (the divergent per-position loop issued ~30K instructions
-        // per wave).
+        // the filter at the chunk's 64 positions, from two register windows of
+        // the staged bytes (the first string's length at p + first_len_at, the
+        // prefix's first 8 bytes at p), all lanes in step: a mask of the
+        // positions that pass.  Then the passing positions are parsed in
+        // order until one is plausible -- a lane parses only its few
+        // candidates, instead of the wave running the parse at every position
+        // some lane's filter passed (the divergent per-position loop issued
+        // ~30K instructions per wave).
         const uint32_t at = static_cast<uint32_t>(clo - r.base);  // LDS offset of the chunk
-        uint64_t mask = cand_mask64(st, at + a.first_len_at + 4);
+        uint64_t mask = 0;
         {
-            // positions inside the chunk whose length field lies inside the wire
+            uint32_t d[kChunk / 4 + 3];
+            const uint32_t o = at + a.first_len_at, sh = o & 3;
+            lds_window(st, o, d);
+#pragma unroll
+            for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            // position j: bytes j .. j + 7 of the shifted window
+            // position j passes when len + j <= lim0 = W - (clo + first_len_at + 8)
+            // (a wrapped sum only adds a candidate: the filter stays necessary)
             const uint64_t need = clo + a.first_len_at + 8;
+            const uint64_t lim0 = need <= W ? W - need : 0;
+#pragma unroll
+            for (int j = 0; j < static_cast<int>(kChunk); ++j) {
+                const int k = j >> 2, s8 = j & 3;
+                const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+                const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+                const uint64_t len = (static_cast<uint64_t>(hi32) << 32) | lo32;
+                mask |= static_cast<uint64_t>(len + j <= lim0) << j;
+            }
+            // positions inside the chunk whose length field lies inside the wire
             const uint64_t jmax = need <= W ? min<uint64_t>(chi - clo, W - need + 1) : 0;
             mask &= jmax >= 64 ? ~0ull : (1ull << jmax) - 1;
+        }
+        if (a.prefix_len && mask) {
+            uint32_t d[kChunk / 4 + 3];
+            const uint32_t sh = at & 3;
+            lds_window(st, at, d);
+#pragma unroll
+            for (int k = 0; k < kChunk / 4 + 2; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
+            const uint64_t pm = k8 == 8 ? ~0ull : (1ull << (8 * k8)) - 1;
+            uint64_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < static_cast<int>(kChunk); ++j) {
+                const int k = j >> 2, s8 = j & 3;
+                const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+                const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+                const uint64_t v = (static_cast<uint64_t>(hi32) << 32) | lo32;
+                keep |= static_cast<uint64_t>(((v ^ a.pre8) & pm) == 0) << j;
+            }
+            mask &= keep;
         }
         const uint64_t passing = mask;
         while (mask) {
@@ -927,8 +911,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     const bool decodes = stream1_decodes(p);
     if (wire_len && !decodes)  // more string fields than it carries: its index replaces ours
         if (int rc = stream1_launch(p, wire, wire_len, n, rec_offs, cols, str_offs, st, s1, gate, s)) return rc;
-    // the indexed decode over the index just built (the timing hook, if armed,
-    // covers the index kernels above only)
+    // the indexed decode over the index just built
     const int rc = srpc_gpu_unpack_var(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch, var, stream);
     if (rc != SRPC_OK) return rc;
     if (wire_len && decodes && sdec && mode != 3) {  // rewrite every output when the gate is set
