@@ -66,7 +66,10 @@ constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint64_t kNone = ~0ull;   // chunk holds no plausible record start
 constexpr uint32_t kStopEnd = 1;    // the walk reached the end of the wire exactly
 constexpr uint32_t kStopBad = 2;    // a record failed to parse at the exit position
-constexpr int kRepairRounds = 3;    // parallel repair rounds before the serial fixer
+#ifndef SRPC_STREAM_ROUNDS
+#define SRPC_STREAM_ROUNDS 2
+#endif
+constexpr int kRepairRounds = SRPC_STREAM_ROUNDS;  // parallel repair rounds before the hand-over
 
 struct StreamArgs {
     uint32_t size[kMaxFields];  // fixed field bytes, 0 = string
