@@ -59,6 +59,9 @@ def layout(recs, nfields):
     # no vtable slot: Quad's struct is its wire body (the tile-copy kernels);
     # Number's fields cover the struct (no read-back of the struct tile)
     ("quad", None, False, 0), ("number", "response", False, 0), ("all", "request", False, 0),
+    # all six kinds, plain and behind a vtable slot, no envelope: the
+    # compile-time layout kernels (rec.hip) for whole tiles, staged ones for the rest
+    ("all", None, False, 0),
     # a struct array 8 bytes off 16-byte alignment: the per-field kernels
     ("quad", None, True, 8), ("all", "request", True, 8)])
 def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
