@@ -233,6 +233,15 @@ public:
                        srpc_unpack_status* d_status = nullptr, void* stream = nullptr) const {
         return srpc_gpu_unpack_aos(_plan, d_wire, wire_len, n, d_records, sizeof(T), _offs.data(), d_status, stream);
     }
+    /// Into fresh objects: every byte no leaf field covers comes from `proto`
+    /// (default: a T{}), so the old array is not read (T trivially copyable
+    /// apart from its vtable pointer, sizeof(T) <= 256).
+    int unpack_records_fresh(const uint8_t* d_wire, uint64_t wire_len, uint64_t n, T* d_records,
+                             const T& proto = T{}, srpc_unpack_status* d_status = nullptr,
+                             void* stream = nullptr) const {
+        return srpc_gpu_unpack_aos_fill(_plan, d_wire, wire_len, n, d_records, sizeof(T), _offs.data(),
+                                        static_cast<const void*>(&proto), d_status, stream);
+    }
 
     /// String schemas: device scratch needed by pack_var / unpack_var for n
     /// records and wire_bytes of wire (pack: wire_cap, unpack: wire_len).

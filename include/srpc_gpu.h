@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 4
+#define SRPC_GPU_ABI_VERSION 5
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -192,6 +192,18 @@ int srpc_gpu_pack_aos(const srpc_plan* plan, const void* d_records, uint64_t rec
 int srpc_gpu_unpack_aos(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
                         void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
                         srpc_unpack_status* d_status, void* stream);
+/* Unpack into FRESH objects (the reference's `std::vector<T> out(n); for
+ * (auto& r : out) r.unpack(...)`, generated T::unpack writing only the leaf
+ * fields of default-constructed objects): as srpc_gpu_unpack_aos, but every
+ * struct byte no leaf field covers is set from h_fill (host, record_stride
+ * bytes: e.g. the bytes of a T{} -- its vtable pointer and the defaults of
+ * members the message does not carry) instead of being kept, so the old
+ * array is never read.  record_stride <= 256 (SRPC_E_UNSUPPORTED otherwise);
+ * h_fill is copied during the call.  Records past a short wire (BOUNDS) are
+ * left as they were, as in srpc_gpu_unpack_aos. */
+int srpc_gpu_unpack_aos_fill(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
+                             void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
+                             const void* h_fill, srpc_unpack_status* d_status, void* stream);
 
 /* ---- variable-length (string) schemas (SRPC_PATH_VAR) ----------------------
  * A string field f is given as its chars d_cols[f] plus n+1 u64 byte offsets

@@ -66,6 +66,7 @@ SIGNATURES = {
     "srpc_group_pack_gather": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _u64, C.c_int, _vp]),
     "srpc_gpu_pack_aos": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, _vp]),
     "srpc_gpu_unpack_aos": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "srpc_gpu_unpack_aos_fill": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _u64, _vp, _vp, _vp, _vp]),
     "srpc_frames_scratch_bytes": (C.c_int, [_u64, C.c_int, C.POINTER(_u64)]),
     "srpc_frames_classify": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64,
                                        _vp]),
@@ -120,7 +121,10 @@ def lib() -> C.CDLL:
                 path = _build.SO
             _preload_torch()
             so = C.CDLL(path, mode=C.RTLD_GLOBAL)
+            ab = bool(os.environ.get("SRPC_GPU_LIB"))
             for name, (res, args) in SIGNATURES.items():
+                if ab and not hasattr(so, name):  # an A/B build older than this table: its symbols only
+                    continue
                 fn = getattr(so, name)
                 fn.restype = res
                 fn.argtypes = args

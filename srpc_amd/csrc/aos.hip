@@ -33,12 +33,15 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "plan.h"
 #include "srpc_gpu.h"
 
 namespace srpc_impl {
 namespace {
+
+constexpr uint32_t kAosFillMax = 256;  // struct bytes srpc_gpu_unpack_aos_fill takes as its fill record
 
 struct AosArgs {
     uint32_t roff[kMaxFields];  // leaf field offset inside the caller's struct
@@ -50,6 +53,9 @@ struct AosArgs {
     bool ident;                 // struct layout == wire layout
     bool cover;                 // the leaf fields cover every byte of the struct
     int32_t boff;               // >= 0: the wire body is struct bytes [boff, boff + wstride) (no prefix)
+    bool fill;                  // unpack into fresh objects: bytes no field covers come from fillw
+    uint32_t fill_at;           // staged kernels: LDS offset of the fill bytes
+    uint32_t fillw[kAosFillMax / 4];  // the fill record (rstride bytes, zero padded)
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -189,6 +195,49 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos_run(const uint8_t* __rest
     for (uint32_t k = 0; k < W / 8; ++k) __builtin_nontemporal_store(v[k], d + k);
 }
 
+// k_unpack_aos_run into fresh objects: a lane writes its WHOLE struct (the
+// run from the wire, every other 8-byte word from the fill record), so the
+// lanes' stores cover whole lines and nothing of the old array is read (the
+// partial-struct writes of k_unpack_aos_run make the memory system read every
+// line they touch: ~64 bytes moved per 40 algorithmic for Quad + vptr).
+template <uint32_t W>
+__global__ __launch_bounds__(kBlock) void k_unpack_aos_run_fill(const uint8_t* __restrict__ wire,
+                                                                uint8_t* __restrict__ recs, AosArgs a, uint64_t n) {
+    const uint64_t e = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(wire + e * W);
+    uint64_t* d = reinterpret_cast<uint64_t*>(recs + e * a.rstride);
+    uint64_t v[W / 8];
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) v[k] = __builtin_nontemporal_load(s + k);
+    // plain stores: the L2 merges a wave's strided 8-byte pieces into whole
+    // lines (non-temporal ones stream out partial lines: 0.27 of peak)
+    const uint32_t b0 = static_cast<uint32_t>(a.boff) >> 3, nw = a.rstride >> 3;  // uniform
+    for (uint32_t k = 0; k < b0; ++k)
+        d[k] = static_cast<uint64_t>(a.fillw[2 * k]) | (static_cast<uint64_t>(a.fillw[2 * k + 1]) << 32);
+#pragma unroll
+    for (uint32_t k = 0; k < W / 8; ++k) d[b0 + k] = v[k];
+    for (uint32_t k = b0 + W / 8; k < nw; ++k)
+        d[k] = static_cast<uint64_t>(a.fillw[2 * k]) | (static_cast<uint64_t>(a.fillw[2 * k + 1]) << 32);
+}
+
+// The fill record into every struct of [0, n) (the per-field fallback's first
+// pass when unpacking into fresh objects): a lane per 4 bytes, or per byte.
+__global__ __launch_bounds__(kBlock) void k_aos_fill(uint8_t* __restrict__ recs, AosArgs a, uint64_t n) {
+    __shared__ uint32_t f[kAosFillMax / 4];
+    if (threadIdx.x < kAosFillMax / 4) f[threadIdx.x] = a.fillw[threadIdx.x];
+    __syncthreads();
+    const uint64_t bytes = n * a.rstride, gs = static_cast<uint64_t>(gridDim.x) * kBlock;
+    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (a.rstride % 4 == 0 && (reinterpret_cast<uintptr_t>(recs) & 3) == 0) {
+        const uint32_t rw = a.rstride / 4;
+        for (uint64_t i = i0; i < bytes / 4; i += gs) reinterpret_cast<uint32_t*>(recs)[i] = f[i % rw];
+    } else {
+        const uint8_t* fb = reinterpret_cast<const uint8_t*>(f);
+        for (uint64_t i = i0; i < bytes; i += gs) recs[i] = fb[i % a.rstride];
+    }
+}
+
 // The run kernels for wire bodies of 8, 16, 24 or 32 bytes (8-byte aligned
 // struct array, stride and body offset), else false.
 bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
@@ -202,6 +251,8 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
     if (a.wstride == Wb) {                                                                                       \
         if (pack) launch(k_pack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, a.rstride, \
                          boff, dst, n);                                                                          \
+        else if (a.fill) launch(k_unpack_aos_run_fill<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s,  \
+                                src, dst, a, n);                                                         \
         else launch(k_unpack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, dst,         \
                     a.rstride, boff, n);                                                                         \
         return true;                                                                                             \
@@ -316,7 +367,23 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos_staged(AosArgs a, const u
     const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(a.R, n - rbase));
     uint8_t* simg = lds + a.simg;
     uint8_t* g = recs + rbase * a.rstride;
-    if (!a.ident && !a.cover) tile_in(simg, g, nr * a.rstride);  // bytes no field covers are written back as they were
+    if (!a.ident && !a.cover) {
+        if (a.fill) {  // fresh objects: the fill record, repeated (no read of the old structs)
+            uint32_t* fl = reinterpret_cast<uint32_t*>(lds + a.fill_at);
+            if (threadIdx.x < kAosFillMax / 4) fl[threadIdx.x] = a.fillw[threadIdx.x];
+            __syncthreads();
+            const uint32_t tb = nr * a.rstride;
+            if (a.rstride % 4 == 0) {
+                const uint32_t rw = a.rstride / 4;
+                for (uint32_t i = threadIdx.x; i < tb / 4; i += kBlock) reinterpret_cast<uint32_t*>(simg)[i] = fl[i % rw];
+            } else {
+                const uint8_t* fb = lds + a.fill_at;
+                for (uint32_t i = threadIdx.x; i < tb; i += kBlock) simg[i] = fb[i % a.rstride];
+            }
+        } else {
+            tile_in(simg, g, nr * a.rstride);  // bytes no field covers are written back as they were
+        }
+    }
     __syncthreads();  // the template, before wire_in reads it
     wire_in(a, lds, tmpl, mask, wire + rbase * a.wstride, nr * a.wstride, rbase, st);
     __syncthreads();
@@ -341,7 +408,8 @@ uint32_t staged_tiling(AosArgs* a) {
     const uint32_t wimg = (R * a->wstride + 15) & ~15u;
     a->simg = a->ident ? 0 : wimg;
     const uint32_t end = a->ident ? wimg : wimg + ((R * a->rstride + 15) & ~15u);
-    return end + (a->prefix_len ? 2 * a->L : 0);
+    a->fill_at = end + (a->prefix_len ? 2 * a->L : 0);
+    return a->fill_at + (a->fill ? kAosFillMax : 0);
 }
 
 __global__ void k_aos_status(srpc_unpack_status* st, uint32_t flags, uint64_t first_bad) {
@@ -389,6 +457,13 @@ int aos_args(const srpc_plan* p, const void* recs, uint64_t stride, const uint32
     return SRPC_OK;
 }
 
+// A/B switch (SRPC_AOS_FILL_STAGED=1 at load): fresh-object unpacks of run
+// layouts take the staged kernels instead of k_unpack_aos_run_fill.
+const bool g_aos_fill_staged = [] {
+    const char* e = std::getenv("SRPC_AOS_FILL_STAGED");
+    return e && e[0] == '1';
+}();
+
 // A/B switch (SRPC_AOS_UNSTAGED=1 in the environment at load): the per-field kernels only.
 const bool g_aos_unstaged = [] {
     const char* e = std::getenv("SRPC_AOS_UNSTAGED");
@@ -430,12 +505,17 @@ int srpc_gpu_pack_aos(const srpc_plan* p, const void* d_records, uint64_t record
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
-int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
-                        void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
-                        srpc_unpack_status* d_status, void* stream) {
+static int unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_len, uint64_t n, void* d_records,
+                      uint64_t record_stride, const uint32_t* field_offsets, const void* h_fill,
+                      srpc_unpack_status* d_status, void* stream) {
     const TimedCall timed;
     AosArgs a{};
     if (int rc = aos_args(p, d_records, record_stride, field_offsets, &a)) return rc;
+    if (h_fill && !a.ident && !a.cover) {  // a struct the fields cover needs no fill
+        if (record_stride > kAosFillMax) return SRPC_E_UNSUPPORTED;
+        std::memcpy(a.fillw, h_fill, record_stride);
+        a.fill = true;
+    }
     auto s = static_cast<hipStream_t>(stream);
     if (d_status) hipLaunchKernelGGL(k_aos_status, dim3(1), dim3(64), 0, s, d_status, 0u, ~0ull);
     if (n == 0) return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
@@ -449,7 +529,7 @@ int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire
     } else {
         n_fit = n;
     }
-    if (n_fit && !a.ident && !g_aos_unstaged &&
+    if (n_fit && !a.ident && !g_aos_unstaged && !(a.fill && g_aos_fill_staged) &&
         launch_aos_run(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
     if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
@@ -457,15 +537,31 @@ int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire
         const uint64_t tiles = (n_fit + a.R - 1) / a.R;
         if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
         launch(k_unpack_aos_staged, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), lds, s, a, d_wire,
-               static_cast<uint8_t*>(d_records), n_fit, d_status, lds - (a.prefix_len ? 2 * a.L : 0));
+               static_cast<uint8_t*>(d_records), n_fit, d_status, a.fill_at - (a.prefix_len ? 2 * a.L : 0));
     } else if (n_fit) {
         a.R = p->tile_R;
         const uint64_t tiles = (n_fit + a.R - 1) / a.R;
         if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        if (a.fill)  // the per-field kernel writes only the fields: fill every struct first
+            launch(k_aos_fill, dim3(static_cast<uint32_t>(std::min<uint64_t>(tiles, 8192))), dim3(kBlock), 0, s,
+                   static_cast<uint8_t*>(d_records), a, n_fit);
         launch(k_unpack_aos, dim3(static_cast<uint32_t>(tiles)), dim3(kBlock), static_cast<uint32_t>(p->tile_lds), s, a,
                d_wire, static_cast<uint8_t*>(d_records), n_fit, d_status);
     }
     return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
+}
+
+int srpc_gpu_unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
+                        void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
+                        srpc_unpack_status* d_status, void* stream) {
+    return unpack_aos(p, d_wire, wire_len, n, d_records, record_stride, field_offsets, nullptr, d_status, stream);
+}
+
+int srpc_gpu_unpack_aos_fill(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_len, uint64_t n,
+                             void* d_records, uint64_t record_stride, const uint32_t* field_offsets,
+                             const void* h_fill, srpc_unpack_status* d_status, void* stream) {
+    if (!h_fill) return SRPC_E_INVALID;
+    return unpack_aos(p, d_wire, wire_len, n, d_records, record_stride, field_offsets, h_fill, d_status, stream);
 }
 
 }  // extern "C"

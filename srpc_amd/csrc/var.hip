@@ -1022,6 +1022,8 @@ constexpr uint64_t kRtuMinAvg = 40;  // record-tile unpack: smallest average rec
 
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
 typedef uint8_t __attribute__((address_space(3))) lds_u8;
+typedef const uint8_t __attribute__((address_space(3))) lds_u8c;
+typedef const u32x4 __attribute__((address_space(3))) lds_u32x4c;
 
 // A workgroup is resident for the whole batch and takes tiles t, t + G, ...
 // (G = the grid, sized by the host to what the chip holds at once), software
@@ -2025,10 +2027,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
             for (uint32_t c = i; c < nch; c += kBlock) {
                 const uint32_t lo = max(h, 16 * c), hi = min(span, 16 * c + 16);
                 if (lo == 16 * c && hi == 16 * c + 16) {
-                    // image bytes [16c - h, 16c - h + 16) = bytes sh.. of the aligned pair at 16c - h - sh
-                    const uint32_t* w = reinterpret_cast<const uint32_t*>(im + 16 * c - h - sh);
-                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6],
-                                   w7 = w[7];
+                    // image bytes [16c - h, 16c - h + 16) = bytes sh.. of the aligned pair at 16c - h - sh,
+                    // read as two 16-byte LDS quads (ds_read_b128: lanes 16 bytes apart are conflict-free;
+                    // the dword pairs the compiler made of plain reads hit every 16th lane's bank)
+                    const lds_u32x4c* q = reinterpret_cast<const lds_u32x4c*>(
+                        (const lds_u8c*)lds + (L.img_at + s_ioff[si] + 16 * c - h - sh));
+                    const u32x4 qa = q[0], qb = sh ? q[1] : u32x4{0, 0, 0, 0};
+                    const uint32_t w0 = qa.x, w1 = qa.y, w2 = qa.z, w3 = qa.w, w4 = qb.x, w5 = qb.y, w6 = qb.z,
+                                   w7 = qb.w;
                     uint32_t o0, o1, o2, o3;
                     const uint32_t b = sh & 3;
                     switch (sh >> 2) {  // uniform

@@ -197,6 +197,18 @@ class GpuPacker:
                                                     self._offsets(field_offsets), _dptr(status), _stream(stream)),
                      "srpc_gpu_unpack_aos")
 
+    def unpack_aos_fill(self, wire, wire_len: int, n: int, records, record_stride: int,
+                        field_offsets: Sequence[int], fill: bytes, status=None, stream=None) -> int:
+        """As unpack_aos into fresh objects: every struct byte no leaf field
+        covers is set from `fill` (record_stride bytes, e.g. a T{} image)."""
+        if len(fill) != record_stride:
+            raise ValueError("fill must be record_stride bytes")
+        buf = C.create_string_buffer(bytes(fill), record_stride)
+        return check(_lib.lib().srpc_gpu_unpack_aos_fill(self._h, _dptr(wire), wire_len, n, _dptr(records),
+                                                         record_stride, self._offsets(field_offsets), buf,
+                                                         _dptr(status), _stream(stream)),
+                     "srpc_gpu_unpack_aos_fill")
+
     # -- string schemas (SRPC_PATH_VAR) -------------------------------------
     def var_scratch_bytes(self, n: int, wire_bytes: int) -> int:
         """Device scratch for pack_var (wire_bytes = wire_cap) / unpack_var (= wire_len)."""

@@ -109,6 +109,45 @@ def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
         assert np.array_equal(b[:, pad], o[:, pad])
 
 
+@pytest.mark.parametrize("n", [1, 17, 4099, 100_003])
+@pytest.mark.parametrize("schema,envelope,vptr,shift", [
+    ("quad", None, True, 0),          # the run kernel (fields one run behind the vtable slot)
+    ("all", None, True, 0), ("all", "request", True, 0), ("i64_i8", None, True, 0),  # staged kernels
+    ("quad", None, False, 0),         # fields cover the struct: no fill needed
+    ("quad", None, True, 8), ("all", "request", True, 8)])  # per-field kernels (+ a fill pass)
+def test_aos_unpack_into_fresh_objects(n, schema, envelope, vptr, shift):
+    """srpc_gpu_unpack_aos_fill: the leaf fields from the wire, every other
+    struct byte from the fill record (a T{} image), whatever the array held."""
+    kinds = {"quad": [oracle.INT32] * 4,
+             "all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
+             "i64_i8": [oracle.INT64, oracle.INT8]}[schema]
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker.for_request(sch, "Svc_servicer::m") if envelope == "request" else GpuPacker(sch)
+    rng = np.random.default_rng(31 * n + len(kinds))
+    recs = random_records(kinds, n, rng, vptr)
+    stride, offs = layout(recs, len(kinds))
+    cols = [np.ascontiguousarray(recs[f"f{i}"]) for i in range(len(kinds))]
+    want = bytes(oracle.pack(kinds, cols, n, p.prefix))
+    fill = rng.integers(0, 256, stride, dtype=np.uint8).tobytes()
+    t = empty(n * stride + 32)
+    t[shift:shift + n * stride].copy_(torch.from_numpy(
+        random_records(kinds, n, np.random.default_rng(5 + n), vptr).view(np.uint8).reshape(-1).copy()))
+    d_other = t[shift:]
+    st = status_buf()
+    assert p.unpack_aos_fill(dev(np.frombuffer(want, np.uint8)), len(want), n, d_other, stride, offs, fill, st) == 0
+    assert read_status(st) == (0, 2**64 - 1)
+    back = host(d_other, n * stride).view(np.uint8).reshape(n, stride)
+    expect = np.tile(np.frombuffer(fill, np.uint8), (n, 1))
+    for o, k in zip(offs, kinds):
+        expect[:, o:o + oracle.KIND_SIZE[k]] = recs.view(np.uint8).reshape(n, stride)[:, o:o + oracle.KIND_SIZE[k]]
+    cover = sum(oracle.KIND_SIZE[k] for k in kinds) == stride
+    if cover:  # nothing to fill: the fields are the struct
+        expect = recs.view(np.uint8).reshape(n, stride)
+    assert np.array_equal(back, expect)
+    # the bytes after the array are untouched
+    assert host(t, n * stride + 32)[shift + n * stride:].tobytes() == b"\xa5" * (32 - shift)
+
+
 def test_aos_all_kinds_reference_fixture(golden_dir):
     """The reference-built all_kinds.bin from structs instead of columns."""
     z = np.load(os.path.join(golden_dir, "all_kinds_in.npz"))

@@ -138,11 +138,23 @@ def main():
         back.copy_(drecs)
         tu = timeit(lambda: p.unpack_aos(wire, n * p.record_bytes, n, back, dt.itemsize, offs, stream=s))
         ok = ok and torch.equal(back, drecs)
+        fill_row = {}
+        if hasattr(p, "unpack_aos_fill"):
+            # into fresh objects (srpc_gpu_unpack_aos_fill): non-field bytes from
+            # record 0's image; the fields must equal the source's
+            fill = recs[:1].view(np.uint8).tobytes()
+            back.zero_()
+            tf = timeit(lambda: p.unpack_aos_fill(wire, n * p.record_bytes, n, back, dt.itemsize, offs, fill, stream=s))
+            got = back[: m * dt.itemsize].cpu().numpy().view(dt)
+            ok = ok and all(np.array_equal(got[f"f{i}"], recs[f"f{i}"][:m]) for i in range(len(sch.kinds)))
+            if vptr:
+                ok = ok and bool(np.all(got["_v"] == recs["_v"][0]))
+            fill_row = {"unpack_fill_us": round(tf * 1e6, 2), "unpack_fill_frac": round(alg / tf / 8e12, 4)}
         rows.append({"case": name, "path": "aos", "records": n, "record_bytes": p.record_bytes,
                      "struct_bytes": dt.itemsize, "alg_bytes": alg, "pack_us": round(tp * 1e6, 2),
                      "unpack_us": round(tu * 1e6, 2), "pack_GBps": round(alg / tp / 1e9, 1),
                      "unpack_GBps": round(alg / tu / 1e9, 1), "pack_frac": round(alg / tp / 8e12, 4),
-                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok)})
+                     "unpack_frac": round(alg / tu / 8e12, 4), "parity_ok": bool(ok), **fill_row})
 
     def var_case(name, kinds, n, maxlen, prefix=b""):
         if args.only not in name:
@@ -242,6 +254,8 @@ def main():
             f.write(txt)
     for r in rows:
         extra = f'  stream {r["stream_us"]:8.1f} us ({r["stream_frac"]:.3f})' if "stream_us" in r else ""
+        if "unpack_fill_us" in r:
+            extra += f'  unpack_fill {r["unpack_fill_us"]:8.1f} us ({r["unpack_fill_frac"]:.3f})'
         if "generic_pack_frac" in r:
             extra += (f'  generic ({r["generic_pack_frac"]:.3f} / {r["generic_unpack_frac"]:.3f})'
                       f'  rec ({r["rec_pack_frac"]:.3f} / {r["rec_unpack_frac"]:.3f})')
