@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kBlock) void k_xscan_reduce(const T* __restrict__ v
 
 // One workgroup of B threads: exclusive scan of the nb block totals in place,
 // thread t owning a contiguous run of them; *total = their sum.  Each run is
-// read and written 16 words per batch (independent loads in flight: a run of
+// read and written 8 words per batch (independent loads in flight: a run of
 // 32 read word by word, one round trip each, took 17 us).
 template <int B>
 __global__ __launch_bounds__(B) void k_xscan_partials(uint64_t* __restrict__ part, uint64_t nb,
@@ -43,16 +43,16 @@ __global__ __launch_bounds__(B) void k_xscan_partials(uint64_t* __restrict__ par
     __shared__ uint64_t ws[B / 64];
     const uint64_t per = (nb + B - 1) / B;
     const uint64_t lo = min<uint64_t>(threadIdx.x * per, nb), hi = min<uint64_t>(lo + per, nb);
-    // 16 predicated loads per batch: a run of up to 16 (nb <= 16 B) is one
-    // round trip (a run of 13 took a batch of 8 and 5 loads one after another)
     uint64_t s = 0;
-    for (uint64_t b = lo; b < hi; b += 16) {
-        uint64_t v[16];
+    uint64_t b = lo;
+    for (; b + 8 <= hi; b += 8) {
+        uint64_t v[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = b + j < hi ? part[b + j] : 0;
+        for (int j = 0; j < 8; ++j) v[j] = part[b + j];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) s += v[j];
+        for (int j = 0; j < 8; ++j) s += v[j];
     }
+    for (; b < hi; ++b) s += part[b];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t inc = s;
 #pragma unroll
@@ -64,15 +64,21 @@ __global__ __launch_bounds__(B) void k_xscan_partials(uint64_t* __restrict__ par
     __syncthreads();
     uint64_t run = inc - s;
     for (int w = 0; w < wave; ++w) run += ws[w];
-    for (uint64_t b = lo; b < hi; b += 16) {
-        uint64_t v[16];
+    b = lo;
+    for (; b + 8 <= hi; b += 8) {
+        uint64_t v[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = b + j < hi ? part[b + j] : 0;
+        for (int j = 0; j < 8; ++j) v[j] = part[b + j];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (b + j < hi) part[b + j] = run;
+        for (int j = 0; j < 8; ++j) {
+            part[b + j] = run;
             run += v[j];
         }
+    }
+    for (; b < hi; ++b) {
+        const uint64_t x = part[b];
+        part[b] = run;
+        run += x;
     }
     if (threadIdx.x == B - 1) {
         uint64_t t = 0;

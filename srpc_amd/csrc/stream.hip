@@ -67,7 +67,7 @@ constexpr uint64_t kNone = ~0ull;   // chunk holds no plausible record start
 constexpr uint32_t kStopEnd = 1;    // the walk reached the end of the wire exactly
 constexpr uint32_t kStopBad = 2;    // a record failed to parse at the exit position
 #ifndef SRPC_STREAM_ROUNDS
-#define SRPC_STREAM_ROUNDS 2
+#define SRPC_STREAM_ROUNDS 3
 #endif
 constexpr int kRepairRounds = SRPC_STREAM_ROUNDS;  // parallel repair rounds before the hand-over
 

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstring>
 #include <random>
+#include <type_traits>
 #include <vector>
 
 static int g_fail = 0, g_pass = 0;
@@ -107,6 +108,21 @@ static int run(srpc::gpu::batch_packer<T>& bp, size_t n, Fill fill, Eq eq, Emit 
     same = true;
     for (size_t i = 0; same && i < n; ++i) same = eq(out2[i], recs[i]);
     CHECK(same);
+    // into fresh objects: the device array holds garbage, every non-field
+    // byte (the vtable pointer) comes from a T{} (unpack_records_fresh)
+    if (sizeof(T) <= 256) {
+        HIPCHECK(hipMemset(drecs, 0xA5, n * sizeof(T)));
+        std::vector<T> out3(n);
+        const T proto{};
+        CHECK(bp.unpack_records_fresh(dw, want.size(), n, drecs, proto, st) == SRPC_OK);
+        HIPCHECK(hipMemcpy(static_cast<void*>(out3.data()), drecs, n * sizeof(T), hipMemcpyDeviceToHost));
+        same = true;
+        for (size_t i = 0; same && i < n; ++i)
+            same = eq(out3[i], recs[i]) &&
+                   (!std::is_polymorphic_v<T> || std::memcmp(static_cast<const void*>(&out3[i]),
+                                                             static_cast<const void*>(&proto), sizeof(void*)) == 0);
+        CHECK(same);
+    }
     (void)hipFree(drecs);
     for (size_t f = 0; f < hc.col.size(); ++f) { (void)hipFree(dcols[f]); (void)hipFree(dback[f]); }
     (void)hipFree(dw);
