@@ -977,6 +977,23 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t n
         for (uint32_t i = threadIdx.x; i < nflags; i += blockDim.x) bad[16 * i] = 0;
 }
 
+// The single-string walk's per-call state in one launch (was three: the
+// status, the exactness flag and a memset of the long-tile marks, ~4-5 us
+// each on the call's critical path).
+__global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* tile_long, uint64_t ntiles) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (st) {
+            st->flags = 0;
+            st->reserved = 0;
+            st->first_bad_record = ~0ull;
+        }
+        bad[0] = 0;
+    }
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < ntiles;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        tile_long[i] = 0;
+}
+
 // ---- record-tile pack: one pass over the inputs -------------------------------------
 // k_pack_var_rt: a workgroup owns a tile of 256 consecutive records, one per
 // lane, and moves every byte once:
@@ -2390,19 +2407,26 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     const TimedCall timed;
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
-    if (st) {
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr, 0u);
-        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
-    }
-    if (!rec_offs || !cols || !str_offs || !scratch) return SRPC_E_INVALID;
+    // the status is reset on every path before its first reporting kernel --
+    // fused into the paths' own reset launches where they have one
+    bool st_done = !st;
+    auto reset_st = [&]() -> bool {
+        if (!st_done) {
+            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st, nullptr, 0u);
+            st_done = true;
+        }
+        return hipGetLastError() == hipSuccess;
+    };
+    auto fail = [&](int rc) { return reset_st() ? rc : SRPC_E_HIP; };
+    if (!rec_offs || !cols || !str_offs || !scratch) return fail(SRPC_E_INVALID);
     const ScratchLayout L = scratch_layout(p, n, wire_len, true);
-    if (scratch_bytes < L.total) return SRPC_E_CAPACITY;
-    if (!aligned(scratch, 8) || !aligned(rec_offs, 8)) return SRPC_E_ALIGN;
+    if (scratch_bytes < L.total) return fail(SRPC_E_CAPACITY);
+    if (!aligned(scratch, 8) || !aligned(rec_offs, 8)) return fail(SRPC_E_ALIGN);
     for (uint32_t f = 0; f < p->nfields; ++f) {
-        if (!cols[f]) return SRPC_E_INVALID;
-        if (p->size[f] && !aligned(cols[f], p->size[f])) return SRPC_E_ALIGN;
+        if (!cols[f]) return fail(SRPC_E_INVALID);
+        if (p->size[f] && !aligned(cols[f], p->size[f])) return fail(SRPC_E_ALIGN);
         if (p->size[f] == 0 && (!str_offs[f] || !aligned(str_offs[f], 8) || !aligned(cols[f], 16)))
-            return SRPC_E_ALIGN;
+            return fail(SRPC_E_ALIGN);
     }
     const VarArgs a = make_var_args(p, reinterpret_cast<const void* const*>(cols),
                                     reinterpret_cast<const uint64_t* const*>(str_offs));
@@ -2412,7 +2436,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     auto* lens = reinterpret_cast<uint64_t*>(base + L.lens_off);
     auto* spos = reinterpret_cast<uint64_t*>(base + L.spos_off);
     const uint64_t grid = (n + kBlock - 1) / kBlock;
-    if (grid > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+    if (grid > 0x7fffffffull) return fail(SRPC_E_UNSUPPORTED);
     auto* bad = reinterpret_cast<uint32_t*>(base + L.bad_off);
     // record tiles, one pass (default), for batches whose tiles' wire spans fit LDS
     RtuArgs R{};
@@ -2427,21 +2451,24 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
     if (p->var_kernel == 1 &&
         (n == 0 || ((wire_len / n >= kRtuMinAvg || p->var_rt_general) && rtu_layout(p, wire_len / n, &R, &rlds)))) {
         if (n == 0) {
+            if (!reset_st()) return SRPC_E_HIP;
             launch(k_str_offs_zero, dim3(1), dim3(64), 0, s, a);
             return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
         }
-        if (!wire) return SRPC_E_INVALID;
+        if (!wire) return fail(SRPC_E_INVALID);
         auto* look = reinterpret_cast<uint64_t*>(base + L.look_off);
         // ticket + look-back words per tile and per 64-tile block, per string field
         const uint64_t w1 = grid * p->nstrings, w2 = ((grid + 63) / 64) * p->nstrings;
         const uint64_t words = 1 + w1 + w2;
         const uint32_t zgrid = static_cast<uint32_t>(std::min<uint64_t>((words + 255) / 256, 1024));
         if (p->nstrings == 1) {
-            launch(k_zero_u64, dim3(1), dim3(64), 0, s, reinterpret_cast<uint64_t*>(bad), 1ull);
+            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st_done ? nullptr : st, bad, 1u);
+            st_done = true;
             launch(k_unpack_var_rt<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
                    wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad);
             launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
         } else {
+            if (!reset_st()) return SRPC_E_HIP;
             launch(k_zero_u64, dim3(zgrid), dim3(256), 0, s, look, words);
         }
         launch(k_unpack_var_rt<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire, wire_len,
@@ -2450,13 +2477,16 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     if (p->nstrings == 1 && n) {  // single-string fast path: no scan unless a record is not exact
-        if (!wire) return SRPC_E_INVALID;
+        if (!wire) return fail(SRPC_E_INVALID);
         const uint32_t f = a.sfield[0];
         uint32_t len_at = p->prefix_len;  // the u64 length follows the prefix and the fixed fields before it
         for (uint32_t g = 0; g < f; ++g) len_at += p->size[g];
-        hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, nullptr, bad, 1u);
         auto* tile_long = reinterpret_cast<uint32_t*>(base + L.long_off);
-        if (hipMemsetAsync(tile_long, 0, 4 * L.max_tiles, s) != hipSuccess) return SRPC_E_HIP;
+        const uint32_t rgrid = static_cast<uint32_t>(std::min<uint64_t>((L.max_tiles + 255) / 256 + 1, 1024));
+        hipLaunchKernelGGL(k_reset_walk1, dim3(rgrid), dim3(256), 0, s, st_done ? nullptr : st, bad, tile_long,
+                           static_cast<uint64_t>(L.max_tiles));
+        st_done = true;
+        if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
         const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
                               len_at + 8};
         // the walk stages its span as in the multi-string path when it fits
@@ -2478,6 +2508,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
                static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad));
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
+    if (!reset_st()) return SRPC_E_HIP;
     if (n) {
         if (!wire) return SRPC_E_INVALID;
         // stage a workgroup's span when 17/16 of the average span fits 48 KiB
