@@ -59,6 +59,210 @@ def parse():
     return ap.parse_args()
 
 
+def committed_profiles(dom_name: str, n: int) -> dict:
+    """The newest round's committed rocprof evidence for the dominant kernel:
+    profiles/rNN_kernel_stats.csv (rocprofv3 --kernel-trace --stats of this
+    bench) and profiles/rNN_pmc_traffic.json (FETCH_SIZE / WRITE_SIZE passes),
+    NN the highest round that has each file; the file names go into the line."""
+    import csv
+    import glob
+    import re
+
+    out = {"traffic": None, "committed_rocprof_avg_us": None, "kernel_stats_file": None, "pmc_file": None}
+    kname = {"pack": "k_pack_dword", "unpack": "k_unpack_dword"}[dom_name]
+
+    def newest(pattern):
+        files = [f for f in glob.glob(os.path.join(ROOT, "profiles", pattern))
+                 if re.match(r"r\d\d_", os.path.basename(f))]
+        return max(files, key=os.path.basename) if files else None
+
+    stats = newest("r??_kernel_stats.csv")
+    if stats:
+        with open(stats) as f:
+            for row in csv.DictReader(f):
+                if kname in row["Name"]:
+                    out["committed_rocprof_avg_us"] = round(float(row["AverageNs"]) / 1e3, 2)
+                    out["kernel_stats_file"] = os.path.relpath(stats, ROOT)
+                    break
+    pmc = newest("r??_pmc_traffic.json")
+    if pmc:
+        with open(pmc) as f:
+            pm = json.load(f)
+        ent = pm.get("kernels", {}).get(dom_name)
+        if ent and pm.get("records") == n:
+            out["traffic"] = ent.get("hbm_bytes_per_launch")
+            out["pmc_file"] = os.path.relpath(pmc, ROOT)
+    return out
+
+
+def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int = 3) -> dict:
+    """The host-terminated path (north_star: it "starts and ends in host
+    memory", the socket buffers of the reference's transport.hpp:94-123), in
+    both directions, pinned host buffers:
+      pack:   host columns -> H2D -> srpc_gpu_pack -> D2H wire;
+      unpack: host wire -> H2D -> srpc_gpu_unpack -> D2H columns.
+    `serial` runs the three steps on one stream; `pipelined` cuts the batch
+    into `chunks` pieces over three streams (H2D / kernels / D2H) and a ring of
+    `depth` device buffers, so H2D of chunk k+1, the kernel of chunk k and D2H
+    of chunk k-1 overlap (PCIe Gen5 is full duplex).  `link` is the copy
+    engines alone: one direction at a time, then both at once (the duplex
+    ceiling a pipelined leg can reach).  Every leg's output is checked."""
+    import torch
+
+    rb = REC_BYTES
+    cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
+    import srpc_amd
+    main = torch.cuda.current_stream(dev)
+    srpc_amd.fill_splitmix_i32(cols, n, 0x5EED, 0, main)
+    hcols = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(4)]
+    hwire = torch.empty(n * rb, dtype=torch.uint8).pin_memory()
+    hback = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(4)]
+    for h, c in zip(hcols, cols):
+        h.copy_(c)
+    wire = torch.empty(n * rb, dtype=torch.uint8, device=dev)
+    back = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
+    p.pack(cols, n, wire, stream=main)
+    want_wire = wire.cpu()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn):
+        fn()  # first use of this leg's copies
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2] * 1e3
+
+    def leg(ms, moved):
+        return {"ms": round(ms, 3), "wire_GiBps": round(n * rb / 2**30 / (ms / 1e3), 3),
+                "mrecords_per_s": round(n / (ms / 1e3) / 1e6, 1),
+                "pcie_GBps_both_directions": round(moved / (ms / 1e3) / 1e9, 1)}
+
+    moved = 2 * n * rb  # 256 MiB in + 256 MiB out per 16M Quads, either direction
+
+    # -- serial, one stream
+    def serial_pack():
+        with torch.cuda.stream(main):
+            for h, c in zip(hcols, cols):
+                c.copy_(h, non_blocking=True)
+            p.pack(cols, n, wire, stream=main)
+            hwire.copy_(wire, non_blocking=True)
+
+    def serial_unpack():
+        with torch.cuda.stream(main):
+            wire.copy_(hwire, non_blocking=True)
+            p.unpack(wire, n * rb, n, back, stream=main)
+            for h, c in zip(hback, back):
+                h.copy_(c, non_blocking=True)
+
+    out = {"what": "pinned host buffers at both ends; 16M Quads per leg; median of %d" % reps}
+    ms = timed(serial_pack)
+    ok_pack = torch.equal(hwire, want_wire)
+    out["serial"] = {"pack": leg(ms, moved)}
+    ms = timed(serial_unpack)
+    ok_unpack = all(torch.equal(a, b) for a, b in zip(hback, hcols))
+    out["serial"]["unpack"] = leg(ms, moved)
+
+    # -- pipelined: three streams, a ring of `depth` chunk buffers
+    per = n // chunks
+    assert per * chunks == n and per % 16 == 0
+    s_in, s_k, s_out = (torch.cuda.Stream(dev) for _ in range(3))
+    rcols = [[torch.empty(per, dtype=torch.int32, device=dev) for _ in range(4)] for _ in range(depth)]
+    rwire = [torch.empty(per * rb, dtype=torch.uint8, device=dev) for _ in range(depth)]
+
+    def pipelined(direction):
+        start = torch.cuda.Event()
+        start.record(main)
+        for st in (s_in, s_k, s_out):
+            st.wait_event(start)
+        ev_k, ev_out = [None] * chunks, [None] * chunks
+        for i in range(chunks):
+            sl = i % depth
+            lo, hi = i * per, (i + 1) * per
+            src_cols, dst_cols = rcols[sl], rcols[sl]
+            if i >= depth:  # the slot's previous chunk: its kernel has read it, its D2H has drained it
+                s_in.wait_event(ev_k[i - depth])
+                s_k.wait_event(ev_out[i - depth])
+            with torch.cuda.stream(s_in):
+                if direction == "pack":
+                    for h, c in zip(hcols, src_cols):
+                        c.copy_(h[lo:hi], non_blocking=True)
+                else:
+                    rwire[sl].copy_(hwire[lo * rb:hi * rb], non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(s_in)
+            s_k.wait_event(ev_in)
+            if direction == "pack":
+                p.pack(src_cols, per, rwire[sl], stream=s_k)
+            else:
+                p.unpack(rwire[sl], per * rb, per, dst_cols, stream=s_k)
+            ev_k[i] = torch.cuda.Event()
+            ev_k[i].record(s_k)
+            s_out.wait_event(ev_k[i])
+            with torch.cuda.stream(s_out):
+                if direction == "pack":
+                    hwire[lo * rb:hi * rb].copy_(rwire[sl], non_blocking=True)
+                else:
+                    for h, c in zip(hback, dst_cols):
+                        h[lo:hi].copy_(c, non_blocking=True)
+                ev_out[i] = torch.cuda.Event()
+                ev_out[i].record(s_out)
+        main.wait_event(ev_out[-1])
+
+    hwire.zero_()
+    ms = timed(lambda: pipelined("pack"))
+    ok_pack = ok_pack and torch.equal(hwire, want_wire)
+    out["pipelined"] = {"pack": leg(ms, moved)}
+    for h in hback:
+        h.zero_()
+    ms = timed(lambda: pipelined("unpack"))
+    ok_unpack = ok_unpack and all(torch.equal(a, b) for a, b in zip(hback, hcols))
+    out["pipelined"]["unpack"] = leg(ms, moved)
+    out["pipelined"].update({"chunks": chunks, "records_per_chunk": per, "ring_depth": depth,
+                             "streams": "H2D / kernels / D2H"})
+
+    # -- the link alone: H2D 256 MiB, D2H 256 MiB, then both at once on two streams
+    def h2d():
+        with torch.cuda.stream(s_in):
+            wire.copy_(hwire, non_blocking=True)
+        main.wait_stream(s_in)
+
+    def d2h():
+        with torch.cuda.stream(s_out):
+            hwire.copy_(wire, non_blocking=True)
+        main.wait_stream(s_out)
+
+    wire.copy_(want_wire.to(dev))
+    hw2 = torch.empty(n * rb, dtype=torch.uint8).pin_memory()
+    w2 = torch.empty(n * rb, dtype=torch.uint8, device=dev)
+
+    def both():
+        with torch.cuda.stream(s_in):
+            w2.copy_(hwire, non_blocking=True)
+        with torch.cuda.stream(s_out):
+            hw2.copy_(wire, non_blocking=True)
+        main.wait_stream(s_in)
+        main.wait_stream(s_out)
+
+    t_h2d, t_d2h, t_both = timed(h2d), timed(d2h), timed(both)
+    out["link"] = {"h2d_GBps": round(n * rb / (t_h2d / 1e3) / 1e9, 1),
+                   "d2h_GBps": round(n * rb / (t_d2h / 1e3) / 1e9, 1),
+                   "duplex_GBps_both_directions": round(moved / (t_both / 1e3) / 1e9, 1),
+                   "duplex_ms_for_one_leg": round(t_both, 3),
+                   "note": "a pipelined leg moves 256 MiB each way: duplex_ms_for_one_leg is its copy floor"}
+    out["pipelined_over_serial"] = {d: round(out["serial"][d]["ms"] / out["pipelined"][d]["ms"], 3)
+                                    for d in ("pack", "unpack")}
+    out["pipelined_over_duplex_floor"] = {d: round(t_both / out["pipelined"][d]["ms"], 3)
+                                          for d in ("pack", "unpack")}
+    out["verified"] = bool(ok_pack and ok_unpack)
+    del cols, back, wire, w2, rcols, rwire
+    return out
+
+
 def cpu_info() -> dict:
     """CPU model and core counts of this host (hardware_concurrency = os.cpu_count())."""
     model = None
@@ -402,29 +606,10 @@ def main() -> None:
                   "sha256": sdig, "scaling": "strong"}
         del scols, sback, swire
 
-    # PCIe-inclusive round trip (host columns -> device -> wire -> host), rank 0 only
+    # PCIe-inclusive legs (host buffers at both ends), rank 0 only
     pcie = None
     if rank == 0 and world == 1 and not args.no_pcie:
-        hcols = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(4)]
-        hwire = torch.empty(n * REC_BYTES, dtype=torch.uint8).pin_memory()
-        for h, c in zip(hcols, cols):
-            h.copy_(c)
-        torch.cuda.synchronize(dev)
-        s0 = torch.cuda.Event(enable_timing=True)
-        s1 = torch.cuda.Event(enable_timing=True)
-        reps = 3
-        s0.record(stream)
-        for _ in range(reps):
-            for h, c in zip(hcols, cols):
-                c.copy_(h, non_blocking=True)
-            p.pack(cols, n, wire, stream=stream)
-            hwire.copy_(wire, non_blocking=True)
-        s1.record(stream)
-        torch.cuda.synchronize(dev)
-        ms = s0.elapsed_time(s1) / reps
-        pcie = {"what": "H2D columns + pack + D2H wire (pinned, one stream)",
-                "ms": round(ms, 3), "wire_GiBps": round(n * REC_BYTES / 2**30 / (ms / 1e3), 3),
-                "mrecords_per_s": round(n / (ms / 1e3) / 1e6, 1)}
+        pcie = pcie_inclusive(p, n, dev)
 
     if rank == 0:
         total_recs = n * world
@@ -436,15 +621,7 @@ def main() -> None:
         frac_cold = None
         if cold:
             frac_cold = round(ALG_BYTES_PER_REC * n / (cold[dom_name] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
-        traffic = rocprof_us = None
-        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(prof):
-            with open(prof) as f:
-                pm = json.load(f)
-            ent = pm.get("kernels", {}).get(dom_name)
-            if ent and pm.get("records") == n:
-                traffic = ent.get("hbm_bytes_per_launch")
-                rocprof_us = round(ent["avg_ns"] / 1e3, 2) if ent.get("avg_ns") else None
+        prof = committed_profiles(dom_name, n)
         line = {
             "metric": "packer GiB/s + Mrecords/s device-resident, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -477,8 +654,12 @@ def main() -> None:
                                    "of the previous call's output); frac_cold: the same kernel after a "
                                    "512 MiB flush",
                          "alg_bytes_per_launch": ALG_BYTES_PER_REC * n,
-                         "traffic": traffic,
-                         "committed_rocprof_avg_us": rocprof_us},
+                         "traffic": prof["traffic"],
+                         "traffic_over_alg": (round(prof["traffic"] / (ALG_BYTES_PER_REC * n), 4)
+                                              if prof["traffic"] else None),
+                         "committed_rocprof_avg_us": prof["committed_rocprof_avg_us"],
+                         "kernel_stats_file": prof["kernel_stats_file"],
+                         "pmc_file": prof["pmc_file"]},
             "verify": verify,
         }
         if gather:

@@ -148,6 +148,7 @@ struct batch_stats {
     uint64_t gpu_requests = 0;       // frames answered from the GPU
     uint64_t fallback_requests = 0;  // frames answered on the CPU (unknown method / shape)
     uint64_t oversize_requests = 0;  // of those, frames longer than the batch buffer
+    uint64_t overflow_batches = 0;   // string-method buckets answered on the CPU: responses past max_response_chars
     uint64_t mixed_batches = 0;      // GPU batches that needed the gather / scatter
     uint64_t h2d_bytes = 0;
     uint64_t d2h_bytes = 0;
@@ -354,6 +355,7 @@ private:
         uint8_t* resp_wire = nullptr;               // packed responses and their index
         uint64_t resp_wire_cap = 0;
         uint64_t* resp_rec = nullptr;
+        uint64_t* h_ends = nullptr;                 // pinned: per response field, offs[0] and offs[n]
     };
     void memset_cols(std::vector<void*> const& cols, std::vector<uint64_t> const& bytes) {
         for (size_t f = 0; f < cols.size(); ++f) check(hipMemsetAsync(cols[f], 0, bytes[f], _s));
@@ -425,6 +427,7 @@ private:
         }
         m.resp_wire = static_cast<uint8_t*>(alloc(m.resp_wire_cap));
         m.resp_rec = static_cast<uint64_t*>(alloc(8 * (_max + 1) + 16));
+        check(hipHostMalloc(reinterpret_cast<void**>(&m.h_ends), 16 * m.resp_string.size() + 16, hipHostMallocDefault));
         uint64_t a = 0, b = 0;
         check_srpc(srpc_plan_var_scratch_bytes(m.in->get(), _max, _cap, &a), "srpc_plan_var_scratch_bytes");
         check_srpc(srpc_plan_var_scratch_bytes(m.out->get(), _max, m.resp_wire_cap, &b), "srpc_plan_var_scratch_bytes");
@@ -439,6 +442,8 @@ private:
             if (p) (void)hipFree(p);
         if (m.resp_wire) (void)hipFree(m.resp_wire);
         if (m.resp_rec) (void)hipFree(m.resp_rec);
+        if (m.h_ends) (void)hipHostFree(m.h_ends);
+        m.h_ends = nullptr;
         m.req_cols.clear();
         m.resp_cols.clear();
         m.req_offs.clear();
@@ -456,7 +461,6 @@ private:
         for (auto& m : _m)
             if (m->var) alloc_var(*m);
         if (_var_scratch_bytes) _d_var_scratch = alloc(_var_scratch_bytes);
-        _d_pack_status = static_cast<srpc_unpack_status*>(alloc(sizeof(srpc_unpack_status)));
         if (any_var_method()) {
             _d_var_rec = alloc(8 * (_max + 1) + 16);
             check(hipHostMalloc(reinterpret_cast<void**>(&_h_out_off), 8 * (_max + 1) + 16, hipHostMallocDefault));
@@ -467,7 +471,9 @@ private:
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_out), out_cap + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_cls), _max + 16, hipHostMallocDefault));
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_counts), 8 * (K + 2) + 16, hipHostMallocDefault));
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_status), 2 * sizeof(srpc_unpack_status), hipHostMallocDefault));
+        // per method: its unpack status [k], its pack status [K + k] (each call
+        // resets its own, so methods never clear each other's)
+        check(hipHostMalloc(reinterpret_cast<void**>(&_h_status), 2 * K * sizeof(srpc_unpack_status), hipHostMallocDefault));
         check(hipMalloc(&_d_in, _cap + 16));
         check(hipMalloc(&_d_offs, 4 * _max + 16));
         check(hipMalloc(&_d_cls, _max + 16));
@@ -477,7 +483,7 @@ private:
         check(hipMalloc(&_d_gather, _cap + 16));
         check(hipMalloc(&_d_resp, out_cap + 16));
         check(hipMalloc(&_d_out, out_cap + 16));
-        check(hipMalloc(&_d_status, sizeof(srpc_unpack_status)));
+        check(hipMalloc(&_d_status, 2 * K * sizeof(srpc_unpack_status)));
         check_srpc(srpc_frames_scratch_bytes(_max, static_cast<int>(K), &_scratch_bytes), "srpc_frames_scratch_bytes");
         check(hipMalloc(&_d_scratch, _scratch_bytes));
         _in_plans.clear();
@@ -530,10 +536,11 @@ private:
                        "srpc_frames_classify");
             check(hipMemcpyAsync(_h_counts, _d_counts, 8 * (K + 2), hipMemcpyDeviceToHost, _s));
             check(hipStreamSynchronize(_s));
-            check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
-            for (auto const& m : _m) {
+            check(hipMemsetAsync(_d_status, 0, 2 * _m.size() * sizeof(srpc_unpack_status), _s));
+            for (size_t k = 0; k < _m.size(); ++k) {
+                auto const& m = _m[k];
                 if (m->var) {
-                    warm_up_var(*m);
+                    warm_up_var(*m, k);
                     continue;
                 }
                 check_srpc(srpc_frames_gather(static_cast<const uint8_t*>(_d_in), static_cast<const uint32_t*>(_d_offs),
@@ -541,7 +548,7 @@ private:
                                               static_cast<uint8_t*>(_d_gather), _s),
                            "srpc_frames_gather");
                 (void)srpc_gpu_unpack(m->in->get(), static_cast<const uint8_t*>(_d_gather), m->fin, 1,
-                                      m->req_cols.data(), _d_status, _s);  // a prefix error on the zero frame: expected
+                                      m->req_cols.data(), _d_status + k, _s);  // a prefix error on the zero frame: expected
                 // the handler's own kernels load their code object on first use
                 // too: it runs on the one zero record (its output is never sent)
                 check_srpc(m->handler(m->req_cols.data(), m->resp_cols.data(), 1, _s), "batch handler (warm-up)");
@@ -559,14 +566,15 @@ private:
             }
             check(hipMemcpyAsync(_h_out, _d_out, out_cap, hipMemcpyDeviceToHost, _s));
             check(hipMemcpyAsync(_h_cls, _d_cls, _max, hipMemcpyDeviceToHost, _s));
-            check(hipMemcpyAsync(_h_status, _d_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
+            check(hipMemcpyAsync(_h_status, _d_status, 2 * _m.size() * sizeof(srpc_unpack_status), hipMemcpyDeviceToHost,
+                                 _s));
             check(hipStreamSynchronize(_s));
         }
     }
     /// One string-method batch on one well-formed request with empty strings
     /// (its prefix, zeros): every kernel of the var path and the handler load
     /// their code objects here, not on the first batch.
-    void warm_up_var(method_entry& m) {
+    void warm_up_var(method_entry& m, size_t k) {
         std::vector<uint8_t> f = be32(static_cast<uint32_t>(m.min_in));
         f.insert(f.end(), m.req_prefix.begin(), m.req_prefix.end());
         f.resize(4 + m.min_in, 0);
@@ -577,17 +585,20 @@ private:
                                           static_cast<const uint32_t*>(_d_index), 1, static_cast<uint8_t*>(_d_gather),
                                           static_cast<uint64_t*>(_d_var_rec), _d_scratch, _scratch_bytes, _s),
                    "srpc_frames_gather_var");
-        run_var_batch(m, 1, m.min_in);
+        run_var_unpack(m, k, 1, m.min_in);
+        run_var_pack(m, k, 1);
         check_srpc(srpc_frames_scatter_var(m.resp_wire, m.resp_rec, static_cast<const uint32_t*>(_d_index), 1,
                                            static_cast<const uint64_t*>(_d_out_off), static_cast<uint8_t*>(_d_out), _s),
                    "srpc_frames_scatter_var");
     }
-    /// unpack_var -> handler -> pack_var over n gathered requests (_d_gather,
-    /// index _d_var_rec, at most wire_len bytes).
-    void run_var_batch(method_entry& m, uint64_t n, uint64_t wire_len) {
+    /// unpack_var -> handler over n gathered requests (_d_gather, index
+    /// _d_var_rec, at most wire_len bytes) of method k, then the first and last
+    /// offsets of every response string field to m.h_ends (checked against the
+    /// columns' sizes before anything reads the chars: run_var_pack).
+    void run_var_unpack(method_entry& m, size_t k, uint64_t n, uint64_t wire_len) {
         check_srpc(srpc_gpu_unpack_var(m.in->get(), static_cast<const uint8_t*>(_d_gather), wire_len, n,
                                        static_cast<const uint64_t*>(_d_var_rec), m.req_cols.data(), m.req_offs.data(),
-                                       _d_status, _d_var_scratch, _var_scratch_bytes, _s),
+                                       _d_status + k, _d_var_scratch, _var_scratch_bytes, _s),
                    "srpc_gpu_unpack_var");
         std::vector<const uint64_t*> req_offs(m.req_offs.begin(), m.req_offs.end());
         var_batch b;
@@ -598,21 +609,38 @@ private:
         b.resp_str_offs = m.resp_offs.data();
         b.resp_cap = m.resp_bytes.data();
         check_srpc(m.vhandler(b, _s), "batch handler");
+        for (size_t f = 0; f < m.resp_offs.size(); ++f) {
+            if (!m.resp_offs[f]) continue;
+            check(hipMemcpyAsync(m.h_ends + 2 * f, m.resp_offs[f], 8, hipMemcpyDeviceToHost, _s));
+            check(hipMemcpyAsync(m.h_ends + 2 * f + 1, m.resp_offs[f] + n, 8, hipMemcpyDeviceToHost, _s));
+        }
+    }
+    /// The handler's response strings of method k fit its columns: offs[0] <=
+    /// offs[n] <= the column's bytes (m.h_ends, after a sync).  The handler
+    /// contract (var_batch) asks for non-decreasing offsets within the column.
+    bool var_responses_fit(method_entry const& m) const {
+        for (size_t f = 0; f < m.resp_offs.size(); ++f) {
+            if (!m.resp_offs[f]) continue;
+            const uint64_t a = m.h_ends[2 * f], e = m.h_ends[2 * f + 1];
+            if (a > e || e > m.resp_bytes[f]) return false;
+        }
+        return true;
+    }
+    void run_var_pack(method_entry& m, size_t k, uint64_t n) {
         std::vector<const uint64_t*> resp_offs(m.resp_offs.begin(), m.resp_offs.end());
         std::vector<const void*> resp_cols(m.resp_cols.begin(), m.resp_cols.end());
         check_srpc(srpc_gpu_pack_var(m.out->get(), resp_cols.data(), resp_offs.data(), n, m.resp_wire, m.resp_wire_cap,
-                                     m.resp_rec, _d_pack_status, _d_var_scratch, _var_scratch_bytes, _s),
+                                     m.resp_rec, _d_status + _m.size() + k, _d_var_scratch, _var_scratch_bytes, _s),
                    "srpc_gpu_pack_var");
     }
 
     void release() {
         for (auto& m : _m)
             if (m->var) free_var(*m);
-        for (void* p : {_d_var_rec, _d_var_scratch, static_cast<void*>(_d_pack_status)})
+        for (void* p : {_d_var_rec, _d_var_scratch})
             if (p) (void)hipFree(p);
         if (_h_out_off) (void)hipHostFree(_h_out_off);
         _d_var_rec = _d_var_scratch = nullptr;
-        _d_pack_status = nullptr;
         _h_out_off = nullptr;
         for (void* p : {_d_in, _d_offs, _d_cls, _d_index, _d_counts, _d_out_off, _d_gather, _d_resp, _d_out,
                         static_cast<void*>(_d_status), _d_scratch})
@@ -656,7 +684,7 @@ private:
         check(hipStreamSynchronize(_s));
         mark("sync1");
         st.classify_seconds += secs(t0);
-        const uint64_t unknown = _h_counts[K + 1];
+        uint64_t unknown = _h_counts[K + 1];
         bool mixed = false, any_var = false;
         for (int k = 0; k < K; ++k) any_var |= _m[static_cast<size_t>(k)]->var && _h_counts[k] > 0;
         uint64_t var_bytes[SRPC_FRAMES_MAX_PLANS] = {};  // payload bytes of each string method's frames
@@ -665,10 +693,14 @@ private:
                 const uint8_t c = _h_cls[i];
                 if (c != SRPC_FRAME_UNKNOWN && _m[c]->var) var_bytes[c] += (i + 1 < nf ? _h_offs[i + 1] : used) - _h_offs[i] - 4;
             }
-        check(hipMemsetAsync(_d_status, 0, sizeof(srpc_unpack_status), _s));
+        check(hipMemsetAsync(_d_status, 0, 2 * static_cast<uint64_t>(K) * sizeof(srpc_unpack_status), _s));
+        bool demoted[SRPC_FRAMES_MAX_PLANS] = {};  // string methods whose answers go to the CPU this batch
         if (any_var) {
-            // string methods first: their responses' sizes place every answer
-            check(hipMemsetAsync(_d_pack_status, 0, sizeof(srpc_unpack_status), _s));
+            // string methods first: their responses' sizes place every answer.
+            // unpack + handler, then the responses' sizes are checked on the
+            // host BEFORE anything reads the response chars: a batch whose
+            // answers do not fit the columns (max_response_chars) is answered
+            // on the CPU server instead, in place (its frames become unknown)
             for (int k = 0; k < K; ++k) {
                 method_entry& m = *_m[static_cast<size_t>(k)];
                 const uint64_t n = _h_counts[k];
@@ -678,9 +710,35 @@ private:
                                                   static_cast<uint8_t*>(_d_gather), static_cast<uint64_t*>(_d_var_rec),
                                                   _d_scratch, _scratch_bytes, _s),
                            "srpc_frames_gather_var");
-                run_var_batch(m, n, var_bytes[k]);
-                mark("var batch");
+                run_var_unpack(m, static_cast<size_t>(k), n, var_bytes[k]);
+                mark("var unpack");
             }
+            check(hipStreamSynchronize(_s));  // the responses' sizes
+            bool any_demoted = false;
+            for (int k = 0; k < K; ++k) {
+                method_entry& m = *_m[static_cast<size_t>(k)];
+                if (!m.var || !_h_counts[k] || var_responses_fit(m)) continue;
+                demoted[k] = any_demoted = true;
+                st.overflow_batches += 1;
+            }
+            if (any_demoted) {
+                for (uint64_t i = 0; i < nf; ++i)
+                    if (_h_cls[i] != SRPC_FRAME_UNKNOWN && demoted[_h_cls[i]]) _h_cls[i] = SRPC_FRAME_UNKNOWN;
+                for (int k = 0; k < K; ++k)
+                    if (demoted[k]) {
+                        unknown += _h_counts[k];
+                        _h_counts[k] = 0;
+                    }
+                check(hipMemcpyAsync(_d_cls, _h_cls, nf, hipMemcpyHostToDevice, _s));
+                check(hipMemcpyAsync(d_counts, _h_counts, 8 * static_cast<uint64_t>(K), hipMemcpyHostToDevice, _s));
+                // the copies read pinned memory the next batch rewrites
+                check(hipStreamSynchronize(_s));
+            }
+            for (int k = 0; k < K; ++k) {
+                method_entry& m = *_m[static_cast<size_t>(k)];
+                if (m.var && _h_counts[k]) run_var_pack(m, static_cast<size_t>(k), _h_counts[k]);
+            }
+            mark("var pack");
             check_srpc(srpc_frames_offsets(_in_plans.data(), _resp_bytes.data(), K, static_cast<const uint8_t*>(_d_cls),
                                            nf, d_idx, d_counts, _var_rec.data(), d_out_off, d_counts + K, _d_scratch,
                                            _scratch_bytes, _s),
@@ -700,7 +758,7 @@ private:
                            "srpc_frames_gather");
                 src = static_cast<const uint8_t*>(_d_gather);
             }
-            check_srpc(srpc_gpu_unpack(m.in->get(), src, n * m.fin, n, m.req_cols.data(), _d_status, _s),
+            check_srpc(srpc_gpu_unpack(m.in->get(), src, n * m.fin, n, m.req_cols.data(), _d_status + k, _s),
                        "srpc_gpu_unpack");
             mark("unpack");
             check_srpc(m.handler(m.req_cols.data(), m.resp_cols.data(), n, _s), "batch handler");
@@ -723,25 +781,28 @@ private:
                                                        n, d_out_off, static_cast<uint8_t*>(_d_out), _s),
                                "srpc_frames_scatter_var");
             }
-            check(hipMemcpyAsync(_h_status + 1, _d_pack_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
             if (unknown) check(hipMemcpyAsync(_h_out_off, d_out_off, 8 * (nf + 1), hipMemcpyDeviceToHost, _s));
             check(hipStreamSynchronize(_s));  // the reply stream's size
             mark("sync_var");
-            if (_h_status[1].flags)
-                throw plan_error("batch_server: string responses exceed max_response_chars", SRPC_E_CAPACITY);
         }
         const uint64_t total = _h_counts[K];
         if (total) check(hipMemcpyAsync(_h_out, _d_out, total, hipMemcpyDeviceToHost, _s));
         mark("d2h_out");
         if (unknown && !var_methods) check(hipMemcpyAsync(_h_cls, _d_cls, nf, hipMemcpyDeviceToHost, _s));
-        check(hipMemcpyAsync(_h_status, _d_status, sizeof(srpc_unpack_status), hipMemcpyDeviceToHost, _s));
+        check(hipMemcpyAsync(_h_status, _d_status, 2 * static_cast<uint64_t>(K) * sizeof(srpc_unpack_status),
+                             hipMemcpyDeviceToHost, _s));
         mark("d2h");
         check(hipStreamSynchronize(_s));
         mark("sync2");
         // classification already matched every prefix and length (and walked
-        // string records to their frame's end): an unpack status here means
-        // the buckets and the plans disagree
-        if (_h_status->flags) throw plan_error("batch_server: classified frame failed to unpack", SRPC_E_INVALID);
+        // string records to their frame's end), and string responses were
+        // checked against their columns before packing: a status here means
+        // the buckets and the plans disagree (an internal invariant)
+        for (int k = 0; k < 2 * K; ++k)
+            if (_h_status[k].flags)
+                throw plan_error(k < K ? "batch_server: classified frame failed to unpack"
+                                       : "batch_server: string responses overran a sized wire",
+                                 SRPC_E_INVALID);
         const double dt = secs(t0);
         if (st.gpu_batches == 0 && st.fallback_requests == 0) st.first_batch_seconds = dt;
         st.gpu_seconds += dt;
@@ -885,7 +946,6 @@ private:
     void* _d_var_rec = nullptr;             // the request index of the bucket being served
     void* _d_var_scratch = nullptr;
     uint64_t _var_scratch_bytes = 0;
-    srpc_unpack_status* _d_pack_status = nullptr;
     uint64_t* _h_out_off = nullptr;
 };
 

@@ -151,3 +151,18 @@ def test_e2e_echo_on_the_cpu_when_not_registered():
     r = _run("--mode", "gpu", "--n", str(n), "--batch", "8192", "--port", "18324", "--echo", "0.25")
     g = _served(r, n)
     assert g["fallback_requests"] == r["traffic"]["echo"] > 5000
+
+
+def test_e2e_echo_responses_past_max_response_chars():
+    """Echo answers (0..41 chars each) into response columns sized for 8
+    chars per request on average: a full batch's answers do not fit, so its
+    echo frames are answered by the CPU server in their places (nothing reads
+    past the columns, the connection keeps serving); square stays on the GPU
+    and every answer is checked by the client."""
+    n = 40_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "8192", "--port", "18325", "--echo", "0.8",
+             "--gpu-methods", "square,echo", "--max-resp-chars", "8")
+    g = _served(r, n)
+    assert g["overflow_batches"] >= 1
+    assert 0 < g["fallback_requests"] <= r["traffic"]["echo"]
+    assert g["gpu_requests"] + g["fallback_requests"] == n

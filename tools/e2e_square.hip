@@ -234,6 +234,7 @@ int main(int argc, char** argv) {
     int64_t oversize = -1;
     double mix = 0, foreign = 0, echo = 0;
     int watchdog_s = 60;
+    uint64_t max_resp_chars = 0;  // 0: var_limits' default
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -252,6 +253,7 @@ int main(int argc, char** argv) {
         else if (a == "--echo") echo = std::stod(next());
         else if (a == "--gpu-methods") gpu_methods = next();
         else if (a == "--watchdog") watchdog_s = std::stoi(next());
+        else if (a == "--max-resp-chars") max_resp_chars = std::stoull(next());
     }
     srpc::message_registry["Number"] = []() -> std::unique_ptr<Number> { return std::make_unique<Number>(); };
     srpc::message_registry["TwoNumbers"] = []() -> std::unique_ptr<TwoNumbers> {
@@ -272,8 +274,11 @@ int main(int argc, char** argv) {
     if (mode == "gpu") {
         gsrv = srpc::gpu::batch_server::single<Number, Number>("Calculator_servicer::square", square_batch, batch, 0,
                                                                &cpu_server);
-        if (gpu_methods.find("echo") != std::string::npos)
-            gsrv->register_var_method<multiple_primitives, multiple_primitives>(echo_fixture::kMethod, echo_batch);
+        if (gpu_methods.find("echo") != std::string::npos) {
+            srpc::gpu::var_limits lim;
+            if (max_resp_chars) lim.max_response_chars = max_resp_chars;
+            gsrv->register_var_method<multiple_primitives, multiple_primitives>(echo_fixture::kMethod, echo_batch, lim);
+        }
         if (gpu_methods.find("all") != std::string::npos) {
             gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::add", binop_batch<ADD>);
             gsrv->register_method<TwoNumbers, Number>("Calculator_servicer::subtract", binop_batch<SUB>);
@@ -460,7 +465,7 @@ int main(int argc, char** argv) {
         "\"traffic\": {\"square\": %llu, \"add\": %llu, \"subtract\": %llu, \"multiply\": %llu, \"divide\": %llu, "
         "\"poison\": %llu, \"oversize\": %llu, \"echo\": %llu, \"mix\": %.4f, \"foreign\": %.4f, \"gpu_methods\": \"%s\"}, "
         "\"gpu\": {\"batches\": %llu, \"mixed_batches\": %llu, \"batch_frames\": %llu, \"buffer_bytes\": %llu, "
-        "\"gpu_requests\": %llu, \"fallback_requests\": %llu, \"oversize_requests\": %llu, "
+        "\"gpu_requests\": %llu, \"fallback_requests\": %llu, \"oversize_requests\": %llu, \"overflow_batches\": %llu, "
         "\"gpu_seconds\": %.6f, \"classify_seconds\": %.6f, \"first_batch_seconds\": %.6f, \"fallback_seconds\": %.6f, \"h2d_bytes\": %llu, \"d2h_bytes\": %llu, "
         "\"recv_seconds\": %.6f, \"send_seconds\": %.6f, \"gpu_requests_per_s\": %.1f}, \"cpu_served\": %zu}\n",
         mode.c_str(), (unsigned long long)n, (got_all && bad == 0) ? "true" : "false", (unsigned long long)bad, secs,
@@ -470,7 +475,8 @@ int main(int argc, char** argv) {
         (unsigned long long)counts[ECHO], mix,
         foreign, gpu_methods.c_str(), (unsigned long long)stats.gpu_batches, (unsigned long long)stats.mixed_batches,
         (unsigned long long)batch, (unsigned long long)buffer_bytes, (unsigned long long)stats.gpu_requests,
-        (unsigned long long)stats.fallback_requests, (unsigned long long)stats.oversize_requests, stats.gpu_seconds,
+        (unsigned long long)stats.fallback_requests, (unsigned long long)stats.oversize_requests,
+        (unsigned long long)stats.overflow_batches, stats.gpu_seconds,
         stats.classify_seconds, stats.first_batch_seconds, stats.fallback_seconds, (unsigned long long)stats.h2d_bytes, (unsigned long long)stats.d2h_bytes,
         stats.recv_seconds, stats.send_seconds,
         stats.gpu_seconds > 0 ? stats.gpu_requests / stats.gpu_seconds : 0.0, cpu_served);
