@@ -95,7 +95,7 @@ def committed_profiles(dom_name: str, n: int) -> dict:
     return out
 
 
-def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int = 3) -> dict:
+def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 32, depth: int = 4) -> dict:
     """The host-terminated path (north_star: it "starts and ends in host
     memory", the socket buffers of the reference's transport.hpp:94-123), in
     both directions, pinned host buffers:
@@ -240,11 +240,13 @@ def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int =
     hw2 = torch.empty(n * rb, dtype=torch.uint8).pin_memory()
     w2 = torch.empty(n * rb, dtype=torch.uint8, device=dev)
 
-    def both():
-        with torch.cuda.stream(s_in):
-            w2.copy_(hwire, non_blocking=True)
-        with torch.cuda.stream(s_out):
-            hw2.copy_(wire, non_blocking=True)
+    def both():  # the same 256 MiB each way, in `chunks` pieces per direction, the two streams interleaved
+        cb = n * rb // chunks
+        for i in range(chunks):
+            with torch.cuda.stream(s_in):
+                w2[i * cb:(i + 1) * cb].copy_(hwire[i * cb:(i + 1) * cb], non_blocking=True)
+            with torch.cuda.stream(s_out):
+                hw2[i * cb:(i + 1) * cb].copy_(wire[i * cb:(i + 1) * cb], non_blocking=True)
         main.wait_stream(s_in)
         main.wait_stream(s_out)
 

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 5
+#define SRPC_GPU_ABI_VERSION 6
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -75,17 +75,27 @@ typedef enum srpc_kind {
 /* Device-side decode status bits (srpc_unpack_status.flags). */
 #define SRPC_STATUS_PREFIX 1u   /* a record's envelope header != the plan's prefix */
 #define SRPC_STATUS_BOUNDS 2u   /* a record (or string) ran past the wire end      */
-#define SRPC_STATUS_STALLED 4u  /* a tile's offset look-back gave up waiting for an
-                                   earlier tile (never expected; results invalid) */
+#define SRPC_STATUS_STALLED 4u  /* srpc_gpu_unpack_var, several string fields: a
+                                   tile's chars-offset look-back polled its
+                                   predecessors past its budget (2^21 polls of
+                                   one word, ~1 s: only a device shared with
+                                   kernels that keep every earlier tile from
+                                   being scheduled).  The outputs are not valid;
+                                   retry the call.  The stream decode
+                                   (srpc_gpu_unpack_var_stream) never waits and
+                                   never reports it. */
 
 /* Written by srpc_gpu_unpack when its d_status argument is non-NULL.
  * Reset by the call itself (stream-ordered) before decoding starts. */
 typedef struct srpc_unpack_status {
     uint32_t flags;             /* OR of SRPC_STATUS_* over the batch          */
     uint32_t reserved;          /* diagnostics of srpc_gpu_unpack_var_stream: bit 0 =
-                                   a mis-speculated chunk was walked again, bit 1 =
-                                   the parallel repair rounds did not settle every
-                                   chunk and the in-order fixer ran            */
+                                   the cursor entered some block at a table slot
+                                   other than the block's speculated start, bit 1 =
+                                   it entered some block where no table slot was
+                                   (that block was walked record by record),
+                                   bits 8-31 = scan waves that walked (saturating);
+                                   0 from every other call                     */
     uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */
 } srpc_unpack_status;
 
@@ -241,13 +251,37 @@ int srpc_gpu_unpack_var(const srpc_plan* plan, const uint8_t* d_wire, uint64_t w
                         uint64_t* const* d_str_offs, srpc_unpack_status* d_status,
                         void* d_scratch, uint64_t scratch_bytes, void* stream);
 
+/* Tile table (ABI 6): for every 256-record tile t of a string batch and
+ * every string field s (in field order), the chars of field s in records
+ * [0, min(256 t, n)): (ceil(n / 256) + 1) * nstrings u64, written by
+ * srpc_gpu_var_tile_table from the batch's string offsets (e.g. the pack
+ * call's input d_str_offs).  Given to srpc_gpu_unpack_var_tiled, every tile
+ * of a schema with several string fields takes its output bases from it
+ * instead of looking back at the tiles before it; each tile checks its own
+ * totals against the table's differences (a wrong table is detected and the
+ * batch decoded again with the look-back, bit-identically).  The table moves
+ * 8 bytes per 256 records per string field beside the record index.
+ * A NULL table: srpc_gpu_unpack_var. */
+int srpc_var_tile_table_words(const srpc_plan* plan, uint64_t n, uint64_t* out);
+int srpc_gpu_var_tile_table(const srpc_plan* plan, const uint64_t* const* d_str_offs, uint64_t n,
+                            uint64_t* d_table, void* stream);
+int srpc_gpu_unpack_var_tiled(const srpc_plan* plan, const uint8_t* d_wire, uint64_t wire_len,
+                              uint64_t n, const uint64_t* d_rec_offs, const uint64_t* d_table,
+                              void* const* d_cols, uint64_t* const* d_str_offs,
+                              srpc_unpack_status* d_status, void* d_scratch, uint64_t scratch_bytes,
+                              void* stream);
+
 /* Unpack n records from a stream with NO record index -- the reference's own
  * decode of a concatenated batch with one shared cursor (buffer::_offset,
  * core.hpp:39; packer.hpp:210-222) -- e.g. the bytes a reference packer
- * appended.  The record starts are found on the device (speculative walks of
- * 512-byte chunks from plausible record starts, each checked against its
- * predecessor's exit, wrong ones walked again in order) and written to
- * d_rec_offs[0..n]; then the records are decoded as by srpc_gpu_unpack_var.
+ * appended.  The record starts are found on the device and written to
+ * d_rec_offs[0..n] with the records decoded as by srpc_gpu_unpack_var: per
+ * 8 KiB block, speculative walks from plausible record starts give a table
+ * from "where the cursor enters the block" to "where it leaves" (records,
+ * chars per string field); an in-order scan of the tables gives every block
+ * its exact entry and output bases; then every block writes its records.
+ * Nothing waits on the device; work is bounded by the stream's bytes on any
+ * input (a cursor position no table holds is walked record by record).
  * The first record the cursor cannot read (prefix mismatch, or a field /
  * string past the end) is reported in *d_status as the first bad record
  * (PREFIX or BOUNDS), as orc_unpack / the reference would meet it; its start

@@ -52,6 +52,9 @@ SIGNATURES = {
     "srpc_gpu_unpack_var": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_gpu_fill_splitmix_i32": (C.c_int, [_vp, C.c_uint32, _u64, _u64, _u64, _vp]),
     "srpc_time_next_call": (C.c_int, [_vp, _vp]),
+    "srpc_var_tile_table_words": (C.c_int, [_vp, _u64, C.POINTER(_u64)]),
+    "srpc_gpu_var_tile_table": (C.c_int, [_vp, _vp, _u64, _vp, _vp]),
+    "srpc_gpu_unpack_var_tiled": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_plan_var_stream_scratch_bytes": (C.c_int, [_vp, _u64, _u64, C.POINTER(_u64)]),
     "srpc_gpu_unpack_var_stream": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_shard_range": (C.c_int, [_u64, C.c_int, C.c_int, C.POINTER(_u64), C.POINTER(_u64)]),

@@ -1,0 +1,1622 @@
+// sdx.hip -- srpc_gpu_unpack_var_stream: decode a concatenated record stream
+// with NO record index, in three phases with no device-side waiting.
+//
+// The reference decodes a batch with ONE shared cursor (buffer::_offset,
+// core.hpp:28-39): every pipe_output advances it (packer.hpp:210-222; nested
+// unpack sharing the buffer as in tests/packer_test.cpp:77-88), so where a
+// record starts is known only once every record before it was read.  Here:
+//
+// 1. k_sx_spec, a workgroup per 8 KiB block of the wire (+ a 2 KiB margin),
+//    staged in LDS by LDS-DMA.  A lane per 32-byte chunk speculates the
+//    chunk's first record start (a filter over its 32 positions from register
+//    windows of the stage, then whole records must parse; of the plausible
+//    starts within a length field's 8 bytes the one with the smallest first
+//    string length) and walks the records starting in the chunk.  Chunks
+//    whose start is their predecessor's exit form segments (scans give any
+//    segment suffix in O(1)).  Then the block's TABLE: for every plausible
+//    position of its first 64 bytes (else the first speculated start), the
+//    chain of records from it to the block end -- exit, records, chars per
+//    string field, stop -- a transfer function from "where the cursor enters"
+//    to "where it leaves".  The speculated start of every chunk goes to
+//    scratch (one byte) for phase 3.  The wire is read once here.
+// 2. the scan of those tables, three small launches:
+//    k_sx_groups  a wave per group of 64 blocks: the group's own table, one
+//                 chain per slot of its first block through its 64 blocks;
+//    k_sx_top     one wave: the groups in order (a group's table entry for the
+//                 cursor's position, held in registers 64 groups at a time),
+//                 every group's entry state; the stream's end: record T where
+//                 it stopped, the status (first bad record, PREFIX / BOUNDS);
+//    k_sx_blocks  a wave per group: every block's entry state (position,
+//                 records before it, chars before it per string field).
+//    A position found in no table (a "miss": the cursor enters a block where
+//    the block did not speculate) is walked record by record from global
+//    memory right there, so the scan is exact on any input and its work is
+//    bounded by the records of the blocks it walks.
+// 3. k_sx_decode, a workgroup per block: the block again (its speculated
+//    chunk starts from scratch, the chunks walked again from LDS), the chain
+//    from the block's exact entry (whole segments jumped), and the block's
+//    records written: rec_offs, fixed columns, str_offs, chars through an LDS
+//    image leaving in aligned 16-byte stores.  Each block's output bases come
+//    from phase 2: no look-back, no wait.
+//
+// Error semantics are orc_unpack's (oracle/packer_oracle.c): the first record
+// that does not parse stops the stream; it is reported (PREFIX or BOUNDS) as
+// the first bad record, every later record BOUNDS; rec_offs[T] = where the
+// stream stopped, rec_offs[T + 1 .. n] = wire_len.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+
+#include "plan.h"
+#include "srpc_gpu.h"
+
+namespace srpc_impl {
+namespace {
+
+constexpr uint32_t kSB = 8192;                   // wire bytes per block (one workgroup)
+constexpr uint32_t kSC = kSB / kBlock;           // 32: wire bytes per speculating lane
+static_assert(kSC % 16 == 0 && kSC <= 64, "16-byte window reads; a chunk's positions fit one 64-bit mask");
+constexpr uint32_t kMargin = 2048;               // staged bytes past the block
+constexpr uint32_t kStage = kSB + kMargin + 32;  // + 16-byte alignment slack on both sides
+constexpr uint32_t kWin = 64;                    // entry window of a block's table (a lane per position)
+constexpr uint32_t kGroup = 64;                  // blocks per group of the scan (a lane per block)
+constexpr int kMaxNC = 3;                        // chars values carried per state (string fields 0..ns-2)
+constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
+constexpr uint32_t kImage = kSB + kMargin + 64;  // chars image of one string field
+constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
+constexpr uint16_t kNoStart = 0xFFFF;
+constexpr uint8_t kNoSpec = 0xFF;
+constexpr int kKeep = 4;                         // table entries per block the scans hold in registers
+constexpr uint64_t kCnt40 = (1ull << 40) - 1;
+constexpr uint32_t kNoPrim = 0xFF;
+constexpr uint32_t kListCap = 5;                 // record starts a 32-byte chunk holds (records >= 8 bytes)
+constexpr uint32_t kDead = 0x81;                 // stop bits of a group-table chain given up (k_sx_groups)
+
+// control words (scratch; k_sx_spec block 0 zeroes them each call)
+constexpr uint32_t kCtlMiss = 0;     // entries found in no table (walked from global memory)
+constexpr uint32_t kCtlOff = 1;      // entries that were not a block's primary slot
+constexpr uint32_t kCtlTailOn = 2;   // the stream stopped before record n: the tail fill runs
+constexpr uint32_t kCtlT = 3;        // ... from record T
+constexpr uint32_t kCtlTot = 4;      // ... str_offs value per string ordinal (kMaxNC + 1 words)
+constexpr uint32_t kCtlWords = 16;
+
+// stop bits: bit 0 = the chain stopped, bits 1-2 = why (SRPC_STATUS_PREFIX / _BOUNDS)
+
+// Per-phase clock (A/B diagnostics, compiled only with -DSRPC_SX_PHASES):
+// thread 0 of every block of k_sx_spec (words 0-7) and k_sx_decode (words
+// 8-15) adds the clock64() cycles between its phase marks into 16 words of
+// its own; srpc_debug_sx_phases points them at a caller's buffer.
+#ifdef SRPC_SX_PHASES
+__device__ unsigned long long* g_sxph = nullptr;
+__device__ unsigned long long g_sxph_blocks = 0;
+#define SXP_BEGIN uint64_t sxp_last_ = clock64();
+#define SXP(i)                                                                                     \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < g_sxph_blocks) {                                      \
+            const uint64_t now_ = clock64();                                                       \
+            g_sxph[static_cast<uint64_t>(blockIdx.x) * 16 + (i)] += now_ - sxp_last_;              \
+            sxp_last_ = now_;                                                                      \
+        }                                                                                          \
+    } while (0)
+#else
+#define SXP_BEGIN
+#define SXP(i)
+#endif
+
+typedef const uint8_t __attribute__((address_space(1))) global_u8;
+typedef uint8_t __attribute__((address_space(3))) lds_u8;
+typedef const uint8_t __attribute__((address_space(3))) lds_u8c;
+typedef const uint32_t __attribute__((address_space(3))) lds_u32c;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct SxArgs {
+    uint32_t size[kMaxFields];   // fixed field bytes, 0 = string
+    uint32_t sord[kMaxFields];   // string ordinal of a string field
+    uint8_t* col[kMaxFields];    // fixed: column; string: chars
+    uint64_t* soff[kMaxFields];  // string: n + 1 chars offsets
+    const uint8_t* prefix;       // device copy (16 zero bytes past the end)
+    uint64_t* rec_offs;
+    uint64_t n, W;
+    uint64_t pre8;               // the prefix's first 8 bytes (zero padded)
+    uint32_t nfields, nstrings, prefix_len, fixed_bytes;
+    uint32_t first_len_at;       // byte offset of the first string's u64 length in a record
+    uint32_t plaus;              // records that must parse from a candidate
+    uint32_t cap;                // record starts a chunk can hold: 1 + kSC / fixed_bytes
+    uint32_t nb, ng;             // blocks, groups
+    uint32_t mode;               // test hooks: 1 = tables hold only the first speculated start, 2 = empty
+                                 // tables, 4 = the exact filter at every position (A/B)
+};
+
+struct SxScratch {
+    uint8_t* spec;   // per chunk: its speculated start minus its first byte, or kNoSpec
+    uint64_t* hdr;   // per block: window mask, first speculated start, slots | primary << 8, 0
+    uint64_t* ent;   // per block, per slot (compact, window order): the chain's E words
+    uint64_t* gent;  // per group, per slot of its first block: the chain to the group's end
+    uint64_t* gp;    // per group: its first block's header words 0-2, then its primary slot's gent entry
+    uint64_t* gin;   // per group: the cursor's state where the group starts (E words)
+    uint64_t* bst;   // per block: the cursor's state where the block starts (E words)
+    uint64_t* ctl;   // kCtlWords
+};
+
+// A chain's result / the cursor's state: position (exit, or the next record
+// start), records, chars of string fields 0..NC-1, stop bits.  Stored as
+// E = 2 + NC words: x, cnt | stop << 40, chars.
+template <int NC>
+struct St {
+    uint64_t x, cnt;
+    uint64_t ch[kMaxNC + 1];
+    uint32_t stop;
+};
+template <int NC>
+constexpr uint32_t ew() { return 2 + NC; }
+
+template <int NC>
+__device__ __forceinline__ void st_store(uint64_t* p, const St<NC>& s) {
+    p[0] = s.x;
+    p[1] = (s.cnt & kCnt40) | (static_cast<uint64_t>(s.stop) << 40);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) p[2 + k] = s.ch[k];
+}
+template <int NC>
+__device__ __forceinline__ St<NC> st_load(const uint64_t* p) {
+    St<NC> s{};
+    s.x = p[0];
+    const uint64_t c = p[1];
+    s.cnt = c & kCnt40;
+    s.stop = static_cast<uint32_t>(c >> 40);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s.ch[k] = p[2 + k];
+    return s;
+}
+// the cursor moves through a block along one of its chains
+template <int NC>
+__device__ __forceinline__ void st_add(St<NC>& s, const St<NC>& e) {
+    s.x = e.x;
+    s.cnt += e.cnt;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s.ch[k] += e.ch[k];
+    s.stop = e.stop;
+}
+// nothing after this state counts: a record failed, or the wire ended
+template <int NC>
+__device__ __forceinline__ bool st_done(const St<NC>& s, uint64_t W) {
+    return (s.stop & 1) || s.x >= W;
+}
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l);
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// ---- wire readers --------------------------------------------------------------
+struct GlobalRd {
+    const uint8_t* w;
+    const uint8_t* pre;  // the prefix (device copy)
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const {
+        uint64_t v;
+        __builtin_memcpy(&v, w + p, 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const { return w[p]; }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const {
+        uint64_t v;
+        __builtin_memcpy(&v, pre + i, 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return pre[i]; }
+};
+// A workgroup's LDS copy of wire bytes [lo, hi) (lds[x] = byte base + x), global
+// memory past it (records that run past the margin).
+struct StagedRd {
+    global_u8* w;
+    lds_u8c* lds;
+    uint64_t base, lo, hi;
+    lds_u8c* pre;  // LDS copy of the prefix, 16-aligned
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const {
+        if (p >= lo && p + 8 <= hi) return u64_lds(p);
+        uint64_t v;
+        __builtin_memcpy(&v, (const uint8_t*)(w + p), 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const { return p >= lo && p < hi ? lds[p - base] : w[p]; }
+    // the sz (1, 2, 4, 8) bytes of a fixed field at p, never a byte past them in global memory
+    __device__ __forceinline__ uint64_t field(uint64_t p, uint32_t sz) const {
+        if (p >= lo && p + sz <= hi) return u64_lds(p);  // the LDS stage has slack past hi
+        switch (sz) {
+        case 1: return w[p];
+        case 2: { uint16_t v; __builtin_memcpy(&v, (const uint8_t*)(w + p), 2); return v; }
+        case 4: { uint32_t v; __builtin_memcpy(&v, (const uint8_t*)(w + p), 4); return v; }
+        default: { uint64_t v; __builtin_memcpy(&v, (const uint8_t*)(w + p), 8); return v; }
+        }
+    }
+    __device__ __forceinline__ uint64_t u64_lds(uint64_t p) const {
+        const uint32_t off = static_cast<uint32_t>(p - base);
+        lds_u32c* q = reinterpret_cast<lds_u32c*>(lds + (off & ~3u));
+        const uint32_t sh = off & 3, w0 = q[0], w1 = q[1], w2 = q[2];
+        return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32) |
+               __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const {
+        lds_u32c* q = reinterpret_cast<lds_u32c*>(pre + i);
+        return (static_cast<uint64_t>(q[1]) << 32) | q[0];
+    }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return pre[i]; }
+    __device__ __forceinline__ bool staged(uint64_t p, uint64_t e) const { return p >= lo && e <= hi && p <= e; }
+};
+// The staged bytes only, for speculation: a read past them yields ~0 (no
+// length fits, no prefix matches), so a candidate whose records run past the
+// stage is not plausible -- a start one byte early whose length reads as
+// len * 256 + a char would otherwise send lanes to global memory.
+struct StageOnlyRd {
+    StagedRd s;
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const { return p >= s.lo && p + 8 <= s.hi ? s.u64(p) : ~0ull; }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const {
+        return p >= s.lo && p < s.hi ? s.lds[p - s.base] : static_cast<uint8_t>(~s.pre[0]);
+    }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const { return s.pre64(i); }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return s.pre8(i); }
+};
+
+// orc_unpack's cursor over one record at p: the position after it, or p with
+// *err set (SRPC_STATUS_PREFIX / _BOUNDS); chars of string fields 0..NC-1
+// added to ch[].
+template <int NC, class Rd>
+__device__ __forceinline__ uint64_t parse_rd(const SxArgs& a, const Rd& r, uint64_t p, uint32_t* err,
+                                             uint64_t (&ch)[kMaxNC + 1]) {
+    const uint64_t W = a.W;
+    *err = 0;
+    if (a.prefix_len) {
+        if (a.prefix_len > W - p) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        uint32_t i = 0;
+        for (; i + 8 <= a.prefix_len; i += 8)
+            if (r.u64(p + i) != r.pre64(i)) {
+                *err = SRPC_STATUS_PREFIX;
+                return p;
+            }
+        for (; i < a.prefix_len; ++i)
+            if (r.u8(p + i) != r.pre8(i)) {
+                *err = SRPC_STATUS_PREFIX;
+                return p;
+            }
+    }
+    uint64_t q = p + a.prefix_len;
+    uint64_t add[kMaxNC + 1] = {};
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < a.nfields; ++f) {
+        const uint32_t sz = a.size[f];
+        if (sz) {
+            if (sz > W - q) {
+                *err = SRPC_STATUS_BOUNDS;
+                return p;
+            }
+            q += sz;
+            continue;
+        }
+        if (8 > W - q) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        const uint64_t len = r.u64(q);
+        q += 8;
+        if (len > W - q) {
+            *err = SRPC_STATUS_BOUNDS;
+            return p;
+        }
+        q += len;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) add[k] += si == static_cast<uint32_t>(k) ? len : 0;
+        ++si;
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) ch[k] += add[k];
+    return q;
+}
+
+// Necessary for a record to parse at p: the prefix's first (up to 8) bytes
+// match and the first string's length fits the wire.
+template <class Rd>
+__device__ __forceinline__ bool filter(const SxArgs& a, const Rd& r, uint64_t p) {
+    const uint64_t W = a.W;
+    if (p > W || a.first_len_at + 8 > W - p) return false;
+    if (a.prefix_len) {
+        const uint32_t k = a.prefix_len < 8 ? a.prefix_len : 8;
+        const uint64_t mask = k == 8 ? ~0ull : (1ull << (8 * k)) - 1;
+        uint64_t v = 0;
+        if (8 <= W - p) v = r.u64(p);
+        else
+            for (uint32_t i = 0; i < k; ++i) v |= static_cast<uint64_t>(r.u8(p + i)) << (8 * i);
+        if (((v ^ a.pre8) & mask) != 0) return false;
+    }
+    return r.u64(p + a.first_len_at) <= W - (p + a.first_len_at + 8);
+}
+
+template <class Rd>
+__device__ __forceinline__ bool plausible(const SxArgs& a, const Rd& r, uint64_t p) {
+    uint64_t ch[kMaxNC + 1];
+    for (uint32_t k = 0; k < a.plaus; ++k) {
+        if (p == a.W) return k > 0;  // the stream may end right after a record
+        uint32_t err;
+        const uint64_t q = parse_rd<0>(a, r, p, &err, ch);
+        if (err) return false;
+        p = q;
+    }
+    return true;
+}
+
+// The N dwords at LDS byte offset o & ~3 of the stage, in 16-byte reads (o
+// mod 16 is the same for every lane: chunks are a multiple of 16 bytes
+// apart, so the dword shift is a uniform switch).
+template <int N>
+__device__ __forceinline__ void lds_window(const uint8_t* st, uint32_t o, uint32_t (&d)[N]) {
+    constexpr int NQ = (N + 3 + 3) / 4;
+    uint32_t w[4 * NQ];
+    typedef const u32x4 __attribute__((address_space(3))) lds_u32x4c;
+    lds_u32x4c* q = reinterpret_cast<lds_u32x4c*>((lds_u8c*)st + (o & ~15u));
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const u32x4 v = q[i];
+        w[4 * i] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+    switch (__builtin_amdgcn_readfirstlane((o >> 2) & 3)) {
+    case 0:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k];
+        break;
+    case 1:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 1];
+        break;
+    case 2:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 2];
+        break;
+    default:
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = w[k + 3];
+        break;
+    }
+}
+
+// Positions of a chunk (LDS offset `at`, wire offset clo, up to chi) that pass
+// the filter, as a mask: the first string's length at p + first_len_at fits
+// the wire, the prefix's first 8 bytes match -- all positions at once from
+// register windows of the stage.
+__device__ __forceinline__ uint64_t chunk_mask(const SxArgs& a, const uint8_t* st, uint32_t at, uint64_t clo,
+                                               uint64_t chi) {
+    const uint64_t W = a.W;
+    uint64_t mask = 0;
+    {
+        uint32_t d[kSC / 4 + 3];
+        const uint32_t o = at + a.first_len_at, sh = o & 3;
+        lds_window(st, o, d);
+#pragma unroll
+        for (int k = 0; k < static_cast<int>(kSC / 4 + 2); ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        // position j passes when len + j <= lim0 = W - (clo + first_len_at + 8)
+        // (a wrapped sum only adds a candidate: the filter stays necessary)
+        const uint64_t need = clo + a.first_len_at + 8;
+        const uint64_t lim0 = need <= W ? W - need : 0;
+#pragma unroll
+        for (int j = 0; j < static_cast<int>(kSC); ++j) {
+            const int k = j >> 2, s8 = j & 3;
+            const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+            const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+            const uint64_t len = (static_cast<uint64_t>(hi32) << 32) | lo32;
+            mask |= static_cast<uint64_t>(len + j <= lim0) << j;
+        }
+        // positions inside the chunk whose length field lies inside the wire
+        const uint64_t jmax = need <= W ? min<uint64_t>(chi - clo, W - need + 1) : 0;
+        mask &= jmax >= 64 ? ~0ull : (1ull << jmax) - 1;
+    }
+    if (a.prefix_len && mask) {
+        uint32_t d[kSC / 4 + 3];
+        const uint32_t sh = at & 3;
+        lds_window(st, at, d);
+#pragma unroll
+        for (int k = 0; k < static_cast<int>(kSC / 4 + 2); ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
+        const uint64_t pm = k8 == 8 ? ~0ull : (1ull << (8 * k8)) - 1;
+        uint64_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < static_cast<int>(kSC); ++j) {
+            const int k = j >> 2, s8 = j & 3;
+            const uint32_t lo32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+            const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], s8) : d[k + 1];
+            const uint64_t v = (static_cast<uint64_t>(hi32) << 32) | lo32;
+            keep |= static_cast<uint64_t>(((v ^ a.pre8) & pm) == 0) << j;
+        }
+        mask &= keep;
+    }
+    return mask;
+}
+
+// chunk_mask for wires under 4 GiB: a length that fits has its four high
+// bytes zero, so only positions whose length field has them zero are
+// candidates (a zero-byte mask of the window: ~5 VALU per dword instead of ~8
+// per position), and each candidate is then tested exactly (its length, the
+// prefix's first 8 bytes) from LDS.  The same mask as chunk_mask.
+__device__ __forceinline__ uint64_t chunk_mask_z(const SxArgs& a, const uint8_t* st, uint32_t at, uint64_t clo,
+                                                 uint64_t chi) {
+    const uint64_t W = a.W;
+    const uint64_t need = clo + a.first_len_at + 8;
+    if (need > W) return 0;
+    const uint64_t lim0 = W - need;
+    const uint64_t jmax = min<uint64_t>(chi - clo, W - need + 1);
+    uint32_t d[kSC / 4 + 3];
+    const uint32_t o = at + a.first_len_at, sh = o & 3;
+    lds_window(st, o, d);
+    // z bit i: byte i of the window (wire offset clo + first_len_at + i) is zero
+    uint64_t z = 0;
+#pragma unroll
+    for (int k = 0; k < static_cast<int>(kSC / 4 + 2); ++k) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const uint32_t nz = ((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v;  // bit 7 of each nonzero byte
+        const uint32_t zb = (~nz >> 7) & 0x01010101u;              // bit 0 of each zero byte
+        z |= static_cast<uint64_t>(((zb * 0x00204081u) >> 21) & 0xFu) << (4 * k);
+    }
+    uint64_t cand = (z >> 4) & (z >> 5) & (z >> 6) & (z >> 7);  // bytes 4..7 of the length at j
+    cand &= jmax >= 64 ? ~0ull : (1ull << jmax) - 1;
+    uint64_t mask = 0;
+    const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
+    const uint64_t pm = k8 == 8 ? ~0ull : (1ull << (8 * k8)) - 1;
+    while (cand) {
+        const uint32_t j = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        if (lds_u64(st, o + j) + j > lim0) continue;
+        if (a.prefix_len && ((lds_u64(st, at + j) ^ a.pre8) & pm)) continue;
+        mask |= 1ull << j;
+    }
+    return mask;
+}
+
+// Exclusive scan of one value per thread over the workgroup (*total = sum).
+__device__ __forceinline__ uint64_t block_xscan(uint64_t x, uint64_t* total, uint64_t* ws) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        before += w < wave ? ws[w] : 0;
+        all += ws[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - x;
+}
+
+// First set bit at index >= i of a 256-bit mask (4 words in LDS), or 256.
+__device__ __forceinline__ uint32_t next_bit(const uint64_t* m, uint32_t i) {
+    if (i >= 256) return 256;
+    uint32_t w = i >> 6;
+    uint64_t v = m[w] & (~0ull << (i & 63));
+    while (!v && ++w < 4) v = m[w];
+    return w < 4 ? 64 * w + __builtin_ctzll(v) : 256;
+}
+
+// A block's chunks in LDS (both the speculation and the decode keep them):
+// per chunk its first start (offset from the block, or none), the position
+// after its records, stop bits, the exclusive scans of records and chars, and
+// 256-bit masks: chunks with a start, segment tails, chunks a chain jumped.
+template <int NC>
+struct Chunks {
+    uint64_t exit[kBlock];
+    uint64_t pch[NC ? NC : 1][kBlock + 1];
+    uint32_t pcnt[kBlock + 1];
+    uint16_t start[kBlock];
+    uint8_t stop[kBlock];
+    uint64_t has[4], tail[4], jump[4];
+    uint64_t ws[kBlock / 64];
+};
+
+// The chain from x (x >= the block start): explicit records are parsed until
+// the walk meets a speculated chunk start, whose segment is then taken whole
+// from the scans (O(1)), and so on.  REC: the explicit starts go to xl (u16
+// offsets from the block, ascending) and jumped chunks to the jump mask.
+template <int NC, bool REC, class Rd>
+__device__ St<NC> walk_chain(const SxArgs& a, const Rd& rd, Chunks<NC>& L, uint64_t b0, uint64_t b1, uint64_t x,
+                             uint16_t* xl, uint32_t* nx) {
+    St<NC> g{};
+    uint64_t q = x;
+    uint32_t ne = 0;
+    while (q < b1) {
+        const uint32_t c = static_cast<uint32_t>((q - b0) / kSC);
+        const uint16_t sc = L.start[c];
+        if (sc != kNoStart && b0 + sc == q) {  // on a speculated segment: jump to its end
+            const uint32_t e = next_bit(L.tail, c);  // the segment's last chunk (always a tail)
+            g.cnt += L.pcnt[e + 1] - L.pcnt[c];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) g.ch[k] += L.pch[k][e + 1] - L.pch[k][c];
+            if (REC) {
+                for (uint32_t j = c; j <= e;) {  // chunks c..e into the jump mask
+                    const uint32_t wi = j >> 6, lo = j & 63, hi = min<uint32_t>(63, e - 64 * wi);
+                    L.jump[wi] |= (hi == 63 ? ~0ull : ((2ull << hi) - 1)) & (~0ull << lo);
+                    j = 64 * (wi + 1);
+                }
+            }
+            q = L.exit[e];
+            if (L.stop[e]) {
+                g.stop = L.stop[e];
+                break;
+            }
+            continue;
+        }
+        uint32_t err;
+        const uint64_t q2 = parse_rd<NC>(a, rd, q, &err, g.ch);
+        if (err) {
+            g.stop = 1 | (err << 1);
+            break;
+        }
+        if (REC) xl[ne] = static_cast<uint16_t>(q - b0);
+        ++ne;
+        ++g.cnt;
+        q = q2;
+    }
+    g.x = q;
+    if (REC) *nx = ne;
+    return g;
+}
+
+// A wave's private LDS copy of a block (+ margin) for the scan's walks: the
+// wire bytes [lo, hi) at stage offset (wire offset - base), the prefix read
+// from global memory (it stays in the caches).
+struct WaveRd {
+    global_u8* w;
+    lds_u8c* lds;
+    uint64_t base, lo, hi;
+    const uint8_t* pre;
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const {
+        if (p >= lo && p + 8 <= hi) {
+            const uint32_t off = static_cast<uint32_t>(p - base);
+            lds_u32c* q = reinterpret_cast<lds_u32c*>(lds + (off & ~3u));
+            const uint32_t sh = off & 3, w0 = q[0], w1 = q[1], w2 = q[2];
+            return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32) |
+                   __builtin_amdgcn_alignbyte(w1, w0, sh);
+        }
+        uint64_t v;
+        __builtin_memcpy(&v, (const uint8_t*)(w + p), 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t u8(uint64_t p) const { return p >= lo && p < hi ? lds[p - base] : w[p]; }
+    __device__ __forceinline__ uint64_t pre64(uint32_t i) const {
+        uint64_t v;
+        __builtin_memcpy(&v, pre + i, 8);
+        return v;
+    }
+    __device__ __forceinline__ uint8_t pre8(uint32_t i) const { return pre[i]; }
+};
+constexpr uint32_t kWaveStage = kSB + kMargin + 32;  // one block + margin, 16-byte aligned either side
+
+// The cursor's way through a block from x when x is in none of its table's
+// slots (a miss): the whole wave copies the block into its LDS stage (16-byte
+// loads, all in flight at once), then every lane that missed walks record by
+// record from there.  Called by every lane of the wave (uniform); lanes with
+// !mine get nothing.
+template <int NC>
+__device__ St<NC> walk_miss(const SxArgs& a, const uint8_t* w, uint8_t* stage, uint64_t b0, uint64_t b1, uint64_t x,
+                            bool mine) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t hi = min<uint64_t>(b1 + kMargin, a.W);
+    const uint64_t A = (reinterpret_cast<uint64_t>(w) + b0) & ~15ull;
+    const uint32_t ng = static_cast<uint32_t>((reinterpret_cast<uint64_t>(w) + hi - A + 15) >> 4);
+    constexpr uint32_t kPer = (kWaveStage / 16 + 63) / 64;
+    u32x4 v[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t gi = lane + 64 * k;
+        if (gi < ng) v[k] = *reinterpret_cast<const u32x4*>(A + 16ull * gi);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t gi = lane + 64 * k;
+        if (gi < ng) *reinterpret_cast<u32x4*>(stage + 16 * gi) = v[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the wave's LDS writes before its reads
+    St<NC> g{};
+    if (!mine) return g;
+    const WaveRd rd{(global_u8*)w, (lds_u8c*)stage, A - reinterpret_cast<uint64_t>(w), b0, hi, a.prefix};
+    uint64_t q = x;
+    while (q < b1) {
+        uint32_t err;
+        const uint64_t q2 = parse_rd<NC>(a, rd, q, &err, g.ch);
+        if (err) {
+            g.stop = 1 | (err << 1);
+            break;
+        }
+        ++g.cnt;
+        q = q2;
+    }
+    g.x = q;
+    return g;
+}
+
+template <int NC>
+__device__ St<NC> walk_global(const SxArgs& a, const uint8_t* w, uint64_t x, uint64_t b1) {
+    const GlobalRd rd{w, a.prefix};
+    St<NC> g{};
+    uint64_t q = x;
+    while (q < b1) {
+        uint32_t err;
+        const uint64_t q2 = parse_rd<NC>(a, rd, q, &err, g.ch);
+        if (err) {
+            g.stop = 1 | (err << 1);
+            break;
+        }
+        ++g.cnt;
+        q = q2;
+    }
+    g.x = q;
+    return g;
+}
+
+// Slot of position x in a block's table (header words h0 = window mask, h1 =
+// the first speculated start): its compact index, or -1 (a miss).
+__device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint32_t nslots, uint64_t b0, uint64_t x) {
+    if (h0) {
+        const uint64_t off = x - b0;
+        if (off < kWin && ((h0 >> off) & 1)) return __builtin_popcountll(h0 & ((1ull << off) - 1));
+        return -1;
+    }
+    return nslots && x == h1 ? 0 : -1;
+}
+
+// Prologue shared by the speculation and the decode: the prefix and the
+// block's bytes [b0, min(b1 + kMargin, W)) in LDS (LDS-DMA), then a barrier.
+__device__ __forceinline__ StagedRd stage_block(const SxArgs& a, const uint8_t* w, uint8_t* st, uint8_t* pre,
+                                                uint64_t b0, uint64_t b1) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t i = tid; i < a.prefix_len + 16; i += kBlock) pre[i] = i < a.prefix_len ? a.prefix[i] : 0;
+    const uint64_t hi = min<uint64_t>(b1 + kMargin, a.W);
+    const uint64_t A = (reinterpret_cast<uint64_t>(w) + b0) & ~15ull;
+    const uint32_t ng = static_cast<uint32_t>((reinterpret_cast<uint64_t>(w) + hi - A + 15) >> 4);
+    for (uint32_t w0 = tid & ~63u; w0 < ng; w0 += kBlock) {
+        const uint32_t gi = w0 + lane;
+        if (gi < ng) {
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(w0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<global_u8*>(A + 16ull * gi), (lds_u8*)(st + 16 * wb), 16,
+                                             0, 0);
+        }
+    }
+    __syncthreads();  // waits for the LDS-DMA and publishes the stage
+    return StagedRd{(global_u8*)w, (lds_u8c*)st, A - reinterpret_cast<uint64_t>(w), b0, hi, (lds_u8c*)pre};
+}
+
+// Chunk tid's records from its start sp (or none): count, the position after
+// them, chars, stop bits, their starts (up to cap, offsets in the chunk).
+template <int NC>
+__device__ __forceinline__ void walk_chunk(const SxArgs& a, const StagedRd& rd, uint64_t sp, uint64_t chi,
+                                           uint32_t* cnt, uint64_t* exit, uint64_t (&ch)[kMaxNC + 1], uint32_t* stop,
+                                           uint8_t* list) {
+    *cnt = 0;
+    *stop = 0;
+    *exit = ~0ull;
+    if (sp == ~0ull) return;
+    uint64_t p = sp;
+    uint32_t k = 0;
+    while (p < chi) {
+        uint32_t err;
+        const uint64_t q = parse_rd<NC>(a, rd, p, &err, ch);
+        if (err) {
+            *stop = 1 | (err << 1);
+            break;
+        }
+        if (list && k < a.cap) list[k] = static_cast<uint8_t>(p % kSC);
+        ++k;
+        p = q;
+    }
+    *cnt = k;
+    *exit = p;
+}
+
+// The chunks' segments: chunk c continues its predecessor's segment when that
+// chunk's exit is c's start (and it did not stop); tails end segments.  Fills
+// L.tail, L.pcnt and L.pch (exclusive scans, totals at [kBlock]).
+template <int NC>
+__device__ __forceinline__ void link_chunks(Chunks<NC>& L, uint64_t b0, uint64_t sp, uint64_t cexit, uint32_t cstop,
+                                            uint32_t ccnt, const uint64_t (&cch)[kMaxNC + 1]) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    bool tail = false;
+    if (sp != ~0ull) {
+        const uint32_t nxt = next_bit(L.has, tid + 1);
+        tail = cstop || nxt >= kBlock || cexit != b0 + L.start[nxt];
+    }
+    const uint64_t tm = __ballot(tail);
+    if (lane == 0) L.tail[tid >> 6] = tm;
+    uint64_t tot;
+    const uint64_t x = block_xscan(ccnt, &tot, L.ws);
+    L.pcnt[tid] = static_cast<uint32_t>(x);
+    if (tid == 0) L.pcnt[kBlock] = static_cast<uint32_t>(tot);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const uint64_t y = block_xscan(cch[k], &tot, L.ws);
+        L.pch[k][tid] = y;
+        if (tid == 0) L.pch[k][kBlock] = tot;
+    }
+    __syncthreads();
+}
+
+// ---- phase 1: speculation and the block tables ----------------------------------
+template <int NC>
+struct SpecLds {
+    alignas(16) uint8_t st[kStage + 16];  // wire bytes [base, base + kStage)
+    alignas(16) uint8_t pre[kMaxPrefix + 16];
+    Chunks<NC> c;
+};
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+    __shared__ SpecLds<NC> L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint64_t b = blockIdx.x;
+    const uint64_t W = a.W;
+    const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
+    SXP_BEGIN
+    if (b == 0 && tid < kCtlWords) S.ctl[tid] = 0;  // this call's counters (read by the later launches)
+    const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);
+    const StageOnlyRd so{rd};
+    SXP(0);
+
+    // speculation: chunk c = tid
+    const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
+    uint64_t sp = ~0ull;  // the chunk's first plausible start
+    if (clo < b1) {
+        if (clo == 0) {
+            sp = 0;  // the stream starts at 0: no speculation
+        } else {
+            const uint32_t at = static_cast<uint32_t>(clo - rd.base);
+            uint64_t mask = W < (1ull << 32) && !(a.mode & 4) ? chunk_mask_z(a, L.st, at, clo, chi)
+                                                               : chunk_mask(a, L.st, at, clo, chi);
+            const uint64_t passing = mask;
+            while (mask) {
+                const uint32_t j = __builtin_ctzll(mask);
+                if (plausible(a, so, clo + j)) {
+                    sp = clo + j;
+                    break;
+                }
+                mask &= mask - 1;
+            }
+            if (sp != ~0ull) {
+                // plausible candidates sp .. sp + 7 inside the chunk: the one
+                // with the smallest first string length (a start 1-3 bytes
+                // early reads the true length shifted up)
+                const uint32_t jb = static_cast<uint32_t>(sp - clo);
+                uint64_t cand = (passing >> (jb + 1)) & 0x7f;
+                uint64_t best = so.u64(sp + a.first_len_at), pick = sp;
+                while (cand) {
+                    const uint64_t q = sp + 1 + __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    const uint64_t l = so.u64(q + a.first_len_at);
+                    if (l < best && plausible(a, so, q)) {
+                        best = l;
+                        pick = q;
+                    }
+                }
+                sp = pick;
+            }
+        }
+    }
+    S.spec[b * kBlock + tid] = sp == ~0ull ? kNoSpec : static_cast<uint8_t>(sp - clo);
+    uint64_t cch[kMaxNC + 1] = {};
+    uint32_t ccnt, cstop;
+    uint64_t cexit;
+    walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+    Chunks<NC>& C = L.c;
+    C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
+    C.exit[tid] = cexit;
+    C.stop[tid] = static_cast<uint8_t>(cstop);
+    const uint64_t hm = __ballot(sp != ~0ull);
+    if (lane == 0) C.has[tid >> 6] = hm;
+    __syncthreads();
+    SXP(1);
+    link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
+    SXP(2);
+
+    // the table (wave 0, lane = window position): every plausible position of
+    // the block's first kWin bytes; a window with none holds the first
+    // speculated start (sF) alone.  The primary slot is sF's: the entry the
+    // speculation itself predicts.
+    if (tid >= 64) return;
+    const uint32_t F = next_bit(C.has, 0);
+    const uint64_t sF = F < kBlock ? b0 + C.start[F] : ~0ull;
+    uint64_t mycand = ~0ull;
+    if (b == 0) {
+        if (lane == 0) mycand = 0;
+    } else if (!(a.mode & 3)) {
+        const uint64_t p = b0 + lane;
+        if (p < b1 && filter(a, so, p) && plausible(a, so, p)) mycand = p;
+    }
+    uint64_t wmask = __ballot(mycand != ~0ull);
+    if (!wmask && lane == 0 && sF != ~0ull && !(a.mode & 2)) mycand = sF;
+    const uint64_t vmask = __ballot(mycand != ~0ull);
+    const uint32_t nslots = __builtin_popcountll(vmask);
+    uint32_t prim = kNoPrim;
+    if (sF != ~0ull && nslots) {
+        if (wmask) {
+            const uint64_t off = sF - b0;  // sF lies in the window whenever the window has a slot
+            if (off < kWin && ((wmask >> off) & 1)) prim = __builtin_popcountll(wmask & ((1ull << off) - 1));
+        } else {
+            prim = 0;
+        }
+    }
+    St<NC> mine{};
+    if (mycand != ~0ull) {
+        mine = walk_chain<NC, false>(a, rd, C, b0, b1, mycand, nullptr, nullptr);
+        const uint32_t k = __builtin_popcountll(vmask & ((1ull << lane) - 1));
+        st_store<NC>(S.ent + (b * kWin + k) * ew<NC>(), mine);
+    }
+    if (lane == 0) {
+        uint64_t* h = S.hdr + 4 * b;
+        h[0] = wmask;
+        h[1] = sF;
+        h[2] = nslots | (static_cast<uint64_t>(prim) << 8);
+        h[3] = 0;
+    }
+    SXP(3);
+}
+
+// ---- phase 2: the scan of the tables ----------------------------------------------
+// A block's header and its first kKeep table entries, one block per lane.
+template <int NC>
+struct Held {
+    uint64_t h0, h1;
+    uint32_t meta;  // slots | primary << 8
+    uint64_t e[kKeep][ew<NC>()];
+    __device__ __forceinline__ void load(const SxScratch& S, uint64_t blk, bool ok) {
+        h0 = 0;
+        h1 = ~0ull;
+        meta = 0;
+        if (!ok) return;
+        const uint64_t* h = S.hdr + 4 * blk;
+        h0 = h[0];
+        h1 = h[1];
+        meta = static_cast<uint32_t>(h[2]);
+        const uint32_t ns = meta & 0xff;
+#pragma unroll
+        for (int k = 0; k < kKeep; ++k)
+            if (static_cast<uint32_t>(k) < ns)
+#pragma unroll
+                for (uint32_t j = 0; j < ew<NC>(); ++j) e[k][j] = S.ent[(blk * kWin + k) * ew<NC>() + j];
+    }
+};
+
+// The cursor's state s through block blk (held in lane l of hv; uniform
+// across the wave or per lane), or, past the held entries, from scratch;
+// in no slot: walked from global memory.  *miss / *off count what happened.
+template <int NC>
+__device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w, const SxScratch& S,
+                                              const Held<NC>& hv, uint32_t l, uint64_t blk, St<NC>& s, bool* miss,
+                                              bool* off, uint8_t* stage, bool may_walk = true) {
+    // the held words of lane l (uniform reads, every lane takes part)
+    const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l);
+    const uint32_t meta = __builtin_amdgcn_readlane(hv.meta, l);
+    uint64_t e[kKeep][ew<NC>()];
+#pragma unroll
+    for (int k = 0; k < kKeep; ++k)
+#pragma unroll
+        for (uint32_t j = 0; j < ew<NC>(); ++j) e[k][j] = rl64(hv.e[k][j], l);
+    const uint64_t b0 = blk * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
+    // a block no record starts in (the cursor is past its end) passes the state on
+    const bool act = !st_done(s, a.W) && s.x < b1;
+    const int idx = act ? slot_of(h0, h1, meta & 0xff, b0, s.x) : 0;
+    if (act && idx < 0 && !may_walk) {  // a chain the caller gives up on instead of walking it
+        s.stop = kDead;
+        return;
+    }
+    St<NC> mw{};
+    if (__ballot(act && idx < 0)) mw = walk_miss<NC>(a, w, stage, b0, b1, s.x, act && idx < 0);
+    if (!act) return;
+    St<NC> t;
+    if (idx >= 0 && idx < kKeep) {
+        uint64_t v[ew<NC>()];
+#pragma unroll
+        for (uint32_t j = 0; j < ew<NC>(); ++j) {
+            v[j] = e[0][j];
+#pragma unroll
+            for (int k = 1; k < kKeep; ++k) v[j] = idx == k ? e[k][j] : v[j];
+        }
+        t = st_load<NC>(v);
+    } else if (idx >= 0) {
+        t = st_load<NC>(S.ent + (blk * kWin + idx) * ew<NC>());
+    } else {
+        t = mw;
+        *miss = true;
+    }
+    if (idx != static_cast<int>((meta >> 8) & 0xff)) *off = true;
+    st_add<NC>(s, t);
+}
+
+// A wave per group: for every slot of the group's first block, the chain
+// through the group's blocks (the group's table, compact in the first block's
+// slot order).  Only the primary slot's chain is walked where it meets no
+// slot; any other chain that does is given up (kDead): a start the block
+// speculated wrongly that runs into positions no table holds would otherwise
+// cost a walk in every later block, and the cursor enters a group there
+// rarely (k_sx_top then takes that group block by block).
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    if (g >= a.ng) return;
+    const uint64_t bf = g * kGroup;
+    const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
+    Held<NC> hv;
+    hv.load(S, bf + lane, lane < nbk);
+    const uint32_t ns0 = __builtin_amdgcn_readlane(hv.meta, 0) & 0xff;
+    const bool act = lane < ns0;
+    St<NC> s{};
+    s.stop = 1;  // lanes past the slots stay put
+    if (act) s = st_load<NC>(S.ent + (bf * kWin + lane) * ew<NC>());
+    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    uint8_t* stage = stages[threadIdx.x >> 6];
+    bool miss = false, off = false;
+    const bool primary = lane == ((__builtin_amdgcn_readlane(hv.meta, 0) >> 8) & 0xff);
+    for (uint32_t j = 1; j < nbk; ++j) {
+        St<NC> t = s;
+        through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, primary);
+        if (act) s = t;
+    }
+    if (act) st_store<NC>(S.gent + (g * kWin + lane) * ew<NC>(), s);
+    // what the in-order pass over the groups reads first, in one record
+    uint64_t* q = S.gp + g * (3 + ew<NC>());
+    const uint32_t meta0 = __builtin_amdgcn_readlane(hv.meta, 0);
+    if (lane == 0) {
+        q[0] = rl64(hv.h0, 0);
+        q[1] = rl64(hv.h1, 0);
+        q[2] = meta0;
+    }
+    if (act && lane == ((meta0 >> 8) & 0xff)) st_store<NC>(q + 3, s);
+}
+
+// One wave: the groups in order.  Each group's entry state (the cursor where
+// the group starts) goes to gin; the group's table entry for the cursor's
+// position is taken from registers (its primary slot) or scratch; a position
+// in no slot of the group's first block, or past that block, takes the group
+// block by block.  Then the stream's end: T, rec_offs[T], str_offs[.][T], the
+// status and the tail fill's parameters for k_sx_decode.
+template <int NC, bool kDecode>
+__global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                               srpc_unpack_status* st) {
+    constexpr uint32_t E = ew<NC>();
+    const uint32_t lane = threadIdx.x;
+    const uint64_t W = a.W;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
+    St<NC> s{};
+    bool miss = false, off = false;
+    // lane l: group base + l -- its first block's header and the group's
+    // primary entry (S.gp), the next batch's loaded while this one is walked
+    uint64_t nq[3 + E];
+    auto fetch = [&](uint64_t base) {
+        const uint64_t g = base + lane;
+#pragma unroll
+        for (uint32_t j = 0; j < 3 + E; ++j) nq[j] = g < a.ng ? S.gp[g * (3 + E) + j] : 0;
+    };
+    fetch(0);
+    for (uint64_t base = 0; base < a.ng; base += 64) {
+        const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(64, a.ng - base));
+        const uint64_t g = base + lane;
+        const uint64_t h0 = nq[0], h1 = nq[1];
+        const uint32_t meta = static_cast<uint32_t>(nq[2]);
+        St<NC> pe = st_load<NC>(nq + 3);  // the group's chain from its primary slot (its first block's sF = h1)
+        fetch(base + 64);
+        const bool has_prim = lane < cnt && ((meta >> 8) & 0xff) != kNoPrim;
+        // link k -> k + 1: group k's primary chain enters group k + 1 at its primary
+        const uint64_t next_p = __shfl_down(h1, 1, 64);
+        const uint32_t next_has = __shfl_down(static_cast<uint32_t>(has_prim), 1, 64);
+        const bool link = has_prim && lane + 1 < cnt && next_has && !(pe.stop & 1) && pe.x == next_p;
+        const uint64_t lmask = __ballot(link);
+        // inclusive prefix sums over the batch of the primary chains' records and chars
+        uint64_t icnt = has_prim ? pe.cnt : 0, ich[kMaxNC + 1];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) ich[k] = has_prim ? pe.ch[k] : 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(icnt, d, 64);
+            if (lane >= static_cast<uint32_t>(d)) icnt += y;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const uint64_t z = __shfl_up(ich[k], d, 64);
+                if (lane >= static_cast<uint32_t>(d)) ich[k] += z;
+            }
+        }
+        uint64_t in[E];
+        uint32_t l = 0;
+        while (l < cnt) {
+            const uint64_t gl = base + l;
+            const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l);
+            const uint32_t lmeta = __builtin_amdgcn_readlane(meta, l);
+            const uint32_t lprim = (lmeta >> 8) & 0xff;
+            if (!st_done(s, W) && lprim != kNoPrim && s.x == lh1) {
+                // a run of groups entered at their primaries: l .. m, m the first
+                // group whose primary chain does not lead to the next one's
+                const uint64_t rest = ~lmask & (~0ull << l);
+                const uint32_t m = min<uint32_t>(rest ? __builtin_ctzll(rest) : 63, cnt - 1);
+                // group k in l..m starts at its primary with the records / chars
+                // of the runs before it: s + (exclusive prefix at k - at l)
+                const uint64_t ex_l_cnt = rl64(icnt, l) - rl64(has_prim ? pe.cnt : 0, l);
+                uint64_t ex_l_ch[kMaxNC + 1];
+#pragma unroll
+                for (int k = 0; k < NC; ++k) ex_l_ch[k] = rl64(ich[k], l) - rl64(has_prim ? pe.ch[k] : 0, l);
+                if (lane >= l && lane <= m) {
+                    St<NC> v{};
+                    v.x = h1;
+                    v.cnt = s.cnt + (icnt - pe.cnt) - ex_l_cnt;
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) v.ch[k] = s.ch[k] + (ich[k] - pe.ch[k]) - ex_l_ch[k];
+                    v.stop = 0;
+                    st_store<NC>(in, v);
+                }
+                St<NC> t{};
+                t.x = rl64(pe.x, m);
+                t.cnt = s.cnt + rl64(icnt, m) - ex_l_cnt;
+#pragma unroll
+                for (int k = 0; k < NC; ++k) t.ch[k] = s.ch[k] + rl64(ich[k], m) - ex_l_ch[k];
+                t.stop = __builtin_amdgcn_readlane(pe.stop, m);
+                s = t;
+                l = m + 1;
+                continue;
+            }
+            {
+                uint64_t v[E];
+                st_store<NC>(v, s);
+#pragma unroll
+                for (uint32_t j = 0; j < E; ++j) in[j] = lane == l ? v[j] : in[j];
+            }
+            ++l;
+            if (st_done(s, W)) continue;
+            const uint64_t bf = gl * kGroup;
+            const uint64_t bend = min<uint64_t>(bf + kGroup, a.nb);
+            if (s.x >= min<uint64_t>(bend * kSB, W)) continue;  // the whole group lies inside one record
+            const uint64_t blk = s.x / kSB;
+            int idx = -1;
+            if (blk == bf) idx = slot_of(lh0, lh1, lmeta & 0xff, bf * kSB, s.x);
+            if (idx >= 0) {
+                const St<NC> e = st_load<NC>(S.gent + (gl * kWin + idx) * E);
+                if (e.stop != kDead) {  // (the primary slot's is taken above)
+                    off = true;
+                    st_add<NC>(s, e);
+                    continue;
+                }
+            }
+            // block by block from the cursor's block to the group's end
+            for (uint64_t j = blk; j < bend && !st_done(s, W); ++j) {
+                const uint64_t b0 = j * kSB, b1 = min<uint64_t>(b0 + kSB, W);
+                if (s.x >= b1) continue;
+                const uint64_t* h = S.hdr + 4 * j;
+                const uint64_t m = h[2];
+                const int k = slot_of(h[0], h[1], static_cast<uint32_t>(m & 0xff), b0, s.x);
+                if (k != static_cast<int>((m >> 8) & 0xff)) off = true;
+                if (k >= 0) {
+                    st_add<NC>(s, st_load<NC>(S.ent + (j * kWin + k) * E));
+                } else {
+                    st_add<NC>(s, walk_miss<NC>(a, w, stage, b0, b1, s.x, true));
+                    miss = true;
+                }
+            }
+        }
+        if (lane < cnt)
+#pragma unroll
+            for (uint32_t j = 0; j < E; ++j) S.gin[g * E + j] = in[j];
+    }
+    if (lane != 0) return;
+    if (miss) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlMiss]), 1ull);
+    if (off) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOff]), 1ull);
+    // the stream's end: s.cnt records decode; record T = s.cnt fails (or the wire ends)
+    const uint64_t n = a.n, T = s.cnt;
+    if (kDecode && st && T >= n) {
+        st->flags = 0;
+        st->first_bad_record = ~0ull;
+    }
+    if (T > n) return;  // record n starts in a block: k_sx_decode writes index n
+    uint64_t tot[kMaxNC + 1];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        tot[k] = s.ch[k];
+        sum += s.ch[k];
+    }
+    // the last string field: every byte before s.x is a fixed part or chars
+    tot[NC] = s.x - T * a.fixed_bytes - sum;
+    a.rec_offs[T] = s.x;
+    if (kDecode)
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            if (a.size[f]) continue;
+            const uint32_t si = a.sord[f];
+            uint64_t v = 0;
+#pragma unroll
+            for (int k = 0; k <= NC; ++k) v = si == static_cast<uint32_t>(k) ? tot[k] : v;
+            a.soff[f][T] = v;
+            S.ctl[kCtlTot + si] = v;
+        }
+    if (T < n) {
+        S.ctl[kCtlT] = T;
+        S.ctl[kCtlTailOn] = 1;
+        if (kDecode && st) {
+            const uint32_t kind = (s.stop & 1) ? (s.stop >> 1) & 3 : 0;
+            st->flags = (kind ? kind : SRPC_STATUS_BOUNDS) | (T + 1 < n ? SRPC_STATUS_BOUNDS : 0);
+            st->first_bad_record = T;
+        }
+    }
+}
+
+// A wave per group: every block's entry state, from the group's.
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+    constexpr uint32_t E = ew<NC>();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    if (g >= a.ng) return;
+    const uint64_t bf = g * kGroup;
+    const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
+    Held<NC> hv;
+    hv.load(S, bf + lane, lane < nbk);
+    St<NC> s = st_load<NC>(S.gin + g * E);
+    uint64_t out[E];
+    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    uint8_t* stage = stages[threadIdx.x >> 6];
+    bool miss = false, off = false;
+    for (uint32_t j = 0; j < nbk; ++j) {
+        uint64_t v[E];
+        st_store<NC>(v, s);
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) out[k] = lane == j ? v[k] : out[k];
+        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage);
+    }
+    if (lane < nbk)
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) S.bst[(bf + lane) * E + k] = out[k];
+    if (lane == 0 && miss) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlMiss]), 1ull);
+    if (lane == 0 && off) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOff]), 1ull);
+}
+
+// ---- phase 3: the records of every block ----------------------------------------
+template <int NC>
+struct DecLds {
+    alignas(16) uint8_t st[kStage + 16];
+    alignas(16) uint8_t pre[kMaxPrefix + 16];
+    alignas(16) uint8_t img[kImage + 32];  // chars image; the explicit start list while walking
+    union {
+        struct {  // until the block's records are listed in tbl
+            Chunks<0> c;
+            uint8_t list[kBlock * kListCap];
+        } w;
+        uint32_t loff[kMaxRec + 1];  // then: per local record, a chars offset (field being copied)
+    } u;
+    uint16_t tbl[kMaxRec + 1];  // the block's records in order: offset from the block
+    uint64_t ws[kBlock / 64];
+    uint32_t s_nexp;
+};
+
+template <int NC, bool kDecode>
+__global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                                      srpc_unpack_status* st) {
+    __shared__ DecLds<NC> L;
+    constexpr uint32_t E = ew<NC>();
+    const uint32_t tid = threadIdx.x;
+    const uint64_t b = blockIdx.x;
+    const uint64_t W = a.W, n = a.n;
+    // the tail: records T + 1 .. n when the stream stopped before record n
+    if (S.ctl[kCtlTailOn]) {
+        const uint64_t T = S.ctl[kCtlT];
+        const uint64_t gs = static_cast<uint64_t>(gridDim.x) * kBlock;
+        for (uint64_t r = T + 1 + b * kBlock + tid; r <= n; r += gs) {
+            a.rec_offs[r] = W;
+            if (kDecode)
+                for (uint32_t f = 0; f < a.nfields; ++f)
+                    if (!a.size[f]) a.soff[f][r] = S.ctl[kCtlTot + a.sord[f]];
+        }
+    }
+    if (b == 0 && tid == 0 && st && kDecode) {  // diagnostics (srpc_unpack_status.reserved)
+        const uint64_t miss = S.ctl[kCtlMiss], off = S.ctl[kCtlOff];
+        st->reserved = (off ? 1u : 0u) | (miss ? 2u : 0u) | (static_cast<uint32_t>(min<uint64_t>(miss, 0xffffff)) << 8);
+    }
+    if (b >= a.nb) return;
+    const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
+    // the block's state, its chunks' speculated starts and its bytes all in
+    // flight at once (a block no record of the batch starts in wastes its stage)
+    SXP_BEGIN
+    const St<NC> s = st_load<NC>(S.bst + b * E);
+    const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
+    const uint8_t sb = clo < b1 ? S.spec[b * kBlock + tid] : kNoSpec;
+    const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);
+    SXP(8);
+    const uint64_t x = s.x, R = s.cnt;
+    if ((s.stop & 1) || x >= b1 || R > n) return;  // no record of the batch starts here
+    Chunks<0>& C = L.u.w.c;
+    // every chunk again from its speculated start (phase 1's byte)
+    const uint64_t sp = sb == kNoSpec ? ~0ull : clo + sb;
+    uint64_t cch[kMaxNC + 1] = {};
+    uint32_t ccnt, cstop;
+    uint64_t cexit;
+    walk_chunk<0>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, L.u.w.list + tid * kListCap);
+    C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
+    C.exit[tid] = cexit;
+    C.stop[tid] = static_cast<uint8_t>(cstop);
+    const uint64_t hm = __ballot(sp != ~0ull);
+    if ((tid & 63) == 0) C.has[tid >> 6] = hm;
+    if (tid < 4) C.jump[tid] = 0;
+    __syncthreads();
+    SXP(9);
+    link_chunks<0>(C, b0, sp, cexit, cstop, ccnt, cch);
+    SXP(10);
+
+    // the chain from the block's entry: explicit starts (in the image area
+    // until the table is built) and the chunks it jumped
+    uint16_t* xl = reinterpret_cast<uint16_t*>(L.img);
+    if (tid == 0) {
+        uint32_t ne = 0;
+        (void)walk_chain<0, true>(a, rd, C, b0, b1, x, xl, &ne);
+        L.s_nexp = ne;
+    }
+    __syncthreads();
+    const uint32_t ne = L.s_nexp;
+    // chunk tid: explicit starts inside it (binary search in the ascending
+    // list), then its speculated starts if the chain jumped it
+    uint32_t e0 = 0, e1 = 0;
+    if (ne) {
+        const uint32_t lo16 = tid * kSC, hi16 = lo16 + kSC;
+        uint32_t l = 0, h = ne;
+        while (l < h) {
+            const uint32_t m = (l + h) >> 1;
+            if (xl[m] < lo16) l = m + 1;
+            else h = m;
+        }
+        e0 = l;
+        h = ne;
+        while (l < h) {
+            const uint32_t m = (l + h) >> 1;
+            if (xl[m] < hi16) l = m + 1;
+            else h = m;
+        }
+        e1 = l;
+    }
+    const bool jumped = (C.jump[tid >> 6] >> (tid & 63)) & 1;
+    const uint32_t fc = (e1 - e0) + (jumped ? ccnt : 0);
+    uint64_t tot;
+    const uint32_t fb = static_cast<uint32_t>(block_xscan(fc, &tot, L.ws));
+    for (uint32_t k = e0; k < e1; ++k) L.tbl[fb + (k - e0)] = xl[k];
+    if (jumped)
+        for (uint32_t k = 0; k < ccnt; ++k)
+            L.tbl[fb + (e1 - e0) + k] = static_cast<uint16_t>(tid * kSC + L.u.w.list[tid * kListCap + k]);
+    __syncthreads();
+    const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(tot, kMaxRec));
+    SXP(11);
+
+    // records r = R + k of the batch, up to index n (record n's start)
+    for (uint32_t k = tid; k < nrec; k += kBlock) {
+        const uint64_t r = R + k;
+        if (r > n) break;
+        const uint64_t sr = b0 + L.tbl[k];
+        a.rec_offs[r] = sr;
+        if (!kDecode || r == n) continue;
+        uint64_t pos = sr + a.prefix_len;
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            const uint32_t sz = a.size[f];
+            const uint64_t v = sz ? rd.field(pos, sz) : rd.u64(pos);
+            if (sz) {
+                uint8_t* dst = a.col[f] + r * sz;
+                switch (sz) {
+                case 1: dst[0] = static_cast<uint8_t>(v); break;
+                case 2: *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(v); break;
+                case 4: *reinterpret_cast<uint32_t*>(dst) = static_cast<uint32_t>(v); break;
+                default: *reinterpret_cast<uint64_t*>(dst) = v; break;
+                }
+                pos += sz;
+            } else {
+                pos += 8 + v;
+            }
+        }
+    }
+    SXP(12);
+    if constexpr (kDecode) {
+        // per string field: local offsets (a scan over the block's records),
+        // str_offs, the chars image, aligned stores
+        uint64_t Pbase[kMaxNC + 1];
+        {
+            uint64_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                Pbase[k] = s.ch[k];
+                sum += Pbase[k];
+            }
+            // the last string field: every byte of a record is its fixed part or chars
+            Pbase[NC] = x - R * a.fixed_bytes - sum;
+        }
+        const uint32_t nw = static_cast<uint32_t>(min<uint64_t>(nrec, n - R));  // records written (r < n)
+        const uint32_t per = (nrec + kBlock - 1) / kBlock;                    // contiguous records per lane
+        for (uint32_t f = 0; f < a.nfields; ++f) {
+            if (a.size[f]) continue;
+            const uint32_t si = a.sord[f];
+            uint64_t P = 0;
+#pragma unroll
+            for (int k = 0; k <= NC; ++k) P = si == static_cast<uint32_t>(k) ? Pbase[k] : P;
+            // lengths of this field (strided: lane per record)
+            for (uint32_t k = tid; k < nrec; k += kBlock) {
+                uint64_t pos = b0 + L.tbl[k] + a.prefix_len, len = 0;
+                for (uint32_t g = 0; g <= f; ++g) {
+                    const uint32_t sz = a.size[g];
+                    if (sz) {
+                        pos += sz;
+                        continue;
+                    }
+                    len = rd.u64(pos);
+                    pos += 8 + (g < f ? len : 0);
+                }
+                L.u.loff[k] = k < nw ? static_cast<uint32_t>(len) : 0;
+            }
+            __syncthreads();
+            // contiguous per lane: serial sums, then the block scan
+            uint64_t mysum = 0;
+            const uint32_t k0 = min(tid * per, nrec), k1 = min(k0 + per, nrec);
+            for (uint32_t k = k0; k < k1; ++k) mysum += L.u.loff[k];
+            uint64_t ftot;
+            uint64_t run = block_xscan(mysum, &ftot, L.ws);
+            for (uint32_t k = k0; k < k1; ++k) {
+                const uint32_t len = L.u.loff[k];
+                L.u.loff[k] = static_cast<uint32_t>(run);
+                run += len;
+            }
+            if (tid == 0) L.u.loff[nrec] = static_cast<uint32_t>(ftot);
+            __syncthreads();
+            uint64_t* so = a.soff[f];
+            uint8_t* chars = a.col[f];
+            for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.loff[k];
+            const bool fits = ftot + 32 <= kImage;
+            // each record's chars into the image (or straight to the output)
+            for (uint32_t k = tid; k < nw; k += kBlock) {
+                const uint32_t o = L.u.loff[k], len = L.u.loff[k + 1] - o;
+                if (!len) continue;
+                const uint64_t sr = b0 + L.tbl[k];
+                uint64_t pos = sr + a.prefix_len;
+                for (uint32_t g = 0; g < f; ++g) pos += a.size[g] ? a.size[g] : 8 + rd.u64(pos);
+                pos += 8;
+                if (fits) {
+                    const uint32_t d = 16 + o;
+                    if (rd.staged(pos, pos + len)) {
+                        uint8_t* l0 = reinterpret_cast<uint8_t*>(&L);
+                        lds_copy_run(l0, static_cast<uint32_t>(L.img - l0) + d,
+                                     static_cast<uint32_t>(L.st - l0) + static_cast<uint32_t>(pos - rd.base), len);
+                    } else {
+                        for (uint32_t x8 = 0; x8 < len; x8 += 8) {
+                            const uint32_t kk = min<uint32_t>(8, len - x8);
+                            uint64_t v = 0;
+                            for (uint32_t bb = 0; bb < kk; ++bb) v |= static_cast<uint64_t>(w[pos + x8 + bb]) << (8 * bb);
+                            lds_put_small(L.img, d + x8, v, kk);
+                        }
+                    }
+                } else {
+                    uint8_t* dst = chars + P + o;
+                    for (uint32_t bb = 0; bb < len; ++bb) dst[bb] = rd.u8(pos + bb);
+                }
+            }
+            __syncthreads();
+            if (fits && ftot) {
+                // chunk c of the output covers image bytes [16c - h, 16c + 16 - h)
+                const uint32_t h = static_cast<uint32_t>(P & 15);
+                const uint64_t gbase = P & ~15ull;
+                const uint8_t* im = L.img + 16;
+                const uint32_t span = h + static_cast<uint32_t>(ftot);
+                const uint32_t nch = (span + 15) >> 4;
+                const uint32_t sh = (16 - h) & 15;
+                for (uint32_t c = tid; c < nch; c += kBlock) {
+                    const uint32_t lo = max(h, 16 * c), hi2 = min(span, 16 * c + 16);
+                    if (lo == 16 * c && hi2 == 16 * c + 16) {
+                        const uint32_t* wd = reinterpret_cast<const uint32_t*>(im + 16 * c - h - sh);
+                        const uint32_t w0 = wd[0], w1 = wd[1], w2 = wd[2], w3 = wd[3], w4 = wd[4], w5 = wd[5],
+                                       w6 = wd[6], w7 = wd[7];
+                        uint32_t o0, o1, o2, o3;
+                        const uint32_t bsh = sh & 3;
+                        switch (sh >> 2) {  // uniform
+                        case 0:
+                            o0 = __builtin_amdgcn_alignbyte(w1, w0, bsh); o1 = __builtin_amdgcn_alignbyte(w2, w1, bsh);
+                            o2 = __builtin_amdgcn_alignbyte(w3, w2, bsh); o3 = __builtin_amdgcn_alignbyte(w4, w3, bsh);
+                            break;
+                        case 1:
+                            o0 = __builtin_amdgcn_alignbyte(w2, w1, bsh); o1 = __builtin_amdgcn_alignbyte(w3, w2, bsh);
+                            o2 = __builtin_amdgcn_alignbyte(w4, w3, bsh); o3 = __builtin_amdgcn_alignbyte(w5, w4, bsh);
+                            break;
+                        case 2:
+                            o0 = __builtin_amdgcn_alignbyte(w3, w2, bsh); o1 = __builtin_amdgcn_alignbyte(w4, w3, bsh);
+                            o2 = __builtin_amdgcn_alignbyte(w5, w4, bsh); o3 = __builtin_amdgcn_alignbyte(w6, w5, bsh);
+                            break;
+                        default:
+                            o0 = __builtin_amdgcn_alignbyte(w4, w3, bsh); o1 = __builtin_amdgcn_alignbyte(w5, w4, bsh);
+                            o2 = __builtin_amdgcn_alignbyte(w6, w5, bsh); o3 = __builtin_amdgcn_alignbyte(w7, w6, bsh);
+                            break;
+                        }
+                        __builtin_nontemporal_store(u32x4{o0, o1, o2, o3},
+                                                    reinterpret_cast<u32x4*>(chars + gbase + 16 * c));
+                    } else {
+                        for (uint32_t xx = lo; xx < hi2; ++xx) chars[gbase + xx] = im[xx - h];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    SXP(13);
+}
+
+__global__ void k_zero_ctl(uint64_t* ctl) {
+    if (threadIdx.x < kCtlWords) ctl[threadIdx.x] = 0;
+}
+
+uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
+
+struct SxLayout {
+    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, total;
+};
+
+SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
+    SxLayout L{};
+    L.nb = (wire_len + kSB - 1) / kSB;
+    L.ng = (L.nb + kGroup - 1) / kGroup;
+    const uint64_t E = 2 + nc;
+    uint64_t o = 0;
+    L.spec = o;
+    o += r256(L.nb * kBlock);
+    L.hdr = o;
+    o += r256(8 * 4 * L.nb);
+    L.ent = o;
+    o += r256(8 * E * kWin * L.nb);
+    L.gent = o;
+    o += r256(8 * E * kWin * L.ng);
+    L.gp = o;
+    o += r256(8 * (3 + E) * L.ng);
+    L.gin = o;
+    o += r256(8 * E * L.ng);
+    L.bst = o;
+    o += r256(8 * E * L.nb);
+    L.ctl = o;
+    o += r256(8 * kCtlWords);
+    L.total = o;
+    return L;
+}
+
+std::atomic<uint32_t> g_sx_mode{0};
+
+bool sx_decodes(const srpc_plan* p) { return p->nstrings <= kMaxNC + 1; }
+
+template <int NC, bool kDecode>
+void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_unpack_status* st, hipStream_t s) {
+    if (a.nb) launch(k_sx_spec<NC>, dim3(a.nb), dim3(kBlock), 0, s, a, wire, S);
+    else hipLaunchKernelGGL(k_zero_ctl, dim3(1), dim3(64), 0, s, S.ctl);
+    const uint32_t gw = (a.ng + kBlock / 64 - 1) / (kBlock / 64);
+    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
+    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st);
+    if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
+    const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
+    launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
+}
+
+}  // namespace
+}  // namespace srpc_impl
+
+// The old decoders (stream.hip: chunk pipeline + indexed decode, sdec.hip,
+// stream1.hip), kept callable for A/B measurements through
+// srpc_debug_stream_force_single(1..6) until they are removed.
+extern "C" int srpc_legacy_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out);
+extern "C" int srpc_legacy_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                                             uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                                             srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes,
+                                             void* stream);
+extern "C" int srpc_legacy_stream_mode();
+
+using namespace srpc_impl;
+
+extern "C" {
+
+int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out) {
+    if (!p || !out || !p->has_string) return SRPC_E_INVALID;
+    uint64_t var = 0, legacy = 0;
+    if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
+    if (int rc = srpc_legacy_var_stream_scratch_bytes(p, n, wire_len, &legacy)) return rc;
+    const uint64_t mine = (sx_decodes(p) ? 0 : r256(var)) + sx_layout(wire_len, sx_decodes(p) ? p->nstrings - 1 : 0).total;
+    *out = std::max(mine, legacy);
+    return SRPC_OK;
+}
+
+int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                               uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                               srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (srpc_legacy_stream_mode())
+        return srpc_legacy_unpack_var_stream(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch,
+                                             scratch_bytes, stream);
+    const TimedCall timed;
+    if (!p || !p->has_string || !rec_offs || !scratch || !cols || !str_offs) return SRPC_E_INVALID;
+    if (wire_len && !wire) return SRPC_E_INVALID;
+    if (!aligned(rec_offs, 8) || !aligned(scratch, 256)) return SRPC_E_ALIGN;
+    uint64_t need = 0;
+    if (int rc = srpc_plan_var_stream_scratch_bytes(p, n, wire_len, &need)) return rc;
+    if (scratch_bytes < need) return SRPC_E_CAPACITY;
+    const bool decode = sx_decodes(p);
+    for (uint32_t f = 0; f < p->nfields && decode; ++f) {
+        if (!cols[f]) return SRPC_E_INVALID;
+        if (p->size[f] && !aligned(cols[f], p->size[f])) return SRPC_E_ALIGN;
+        if (p->size[f] == 0 && (!str_offs[f] || !aligned(str_offs[f], 8) || !aligned(cols[f], 16))) return SRPC_E_ALIGN;
+    }
+    const uint32_t nc = decode ? p->nstrings - 1 : 0;
+    const SxLayout SL = sx_layout(wire_len, nc);
+    // counts travel in 40 bits; positions and chars in full words
+    if (SL.nb > 0x7fffffffull || wire_len >= (1ull << 40) || p->fixed_bytes < 8) return SRPC_E_UNSUPPORTED;
+    uint64_t var = 0;
+    srpc_plan_var_scratch_bytes(p, n, wire_len, &var);
+    auto* base = static_cast<uint8_t*>(scratch) + (decode ? 0 : r256(var));
+    SxScratch S{base + SL.spec,
+                reinterpret_cast<uint64_t*>(base + SL.hdr),
+                reinterpret_cast<uint64_t*>(base + SL.ent),
+                reinterpret_cast<uint64_t*>(base + SL.gent),
+                reinterpret_cast<uint64_t*>(base + SL.gp),
+                reinterpret_cast<uint64_t*>(base + SL.gin),
+                reinterpret_cast<uint64_t*>(base + SL.bst),
+                reinterpret_cast<uint64_t*>(base + SL.ctl)};
+    SxArgs a{};
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        a.size[f] = p->size[f];
+        a.sord[f] = p->size[f] ? 0 : si++;
+        a.col[f] = decode ? static_cast<uint8_t*>(cols[f]) : nullptr;
+        a.soff[f] = decode && !p->size[f] ? str_offs[f] : nullptr;
+    }
+    a.prefix = p->d_prefix;
+    a.rec_offs = rec_offs;
+    a.n = n;
+    a.W = wire_len;
+    a.nfields = p->nfields;
+    a.nstrings = p->nstrings;
+    a.prefix_len = p->prefix_len;
+    a.fixed_bytes = p->fixed_bytes;
+    a.first_len_at = p->prefix_len;
+    for (uint32_t f = 0; f < p->nfields && p->size[f]; ++f) a.first_len_at += p->size[f];
+    a.plaus = p->prefix_len >= 8 ? kPlausPrefixed : kPlausBare;
+    for (uint32_t i = 0; i < 8 && i < p->prefix_len; ++i) a.pre8 |= static_cast<uint64_t>(p->h_prefix[i]) << (8 * i);
+    a.cap = 1 + kSC / p->fixed_bytes;
+    a.nb = static_cast<uint32_t>(SL.nb);
+    a.ng = static_cast<uint32_t>(SL.ng);
+    a.mode = g_sx_mode.load(std::memory_order_relaxed);
+    auto s = static_cast<hipStream_t>(stream);
+    if (!decode) launch_sx<0, false>(a, wire, S, st, s);
+    else if (nc == 0) launch_sx<0, true>(a, wire, S, st, s);
+    else if (nc == 1) launch_sx<1, true>(a, wire, S, st, s);
+    else if (nc == 2) launch_sx<2, true>(a, wire, S, st, s);
+    else launch_sx<3, true>(a, wire, S, st, s);
+    if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+    if (!decode)  // more string fields than a state carries: the indexed decode over the index just built
+        return srpc_gpu_unpack_var(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch, var, stream);
+    return SRPC_OK;
+}
+
+}  // extern "C"
+
+// Test hook (not part of the C ABI in include/), bits: 1 = block tables hold
+// only the first speculated start (every other entry is walked from global
+// memory), 2 = empty tables (every block entered is walked), 4 = the
+// speculation's exact filter at every position instead of zero-byte
+// candidates; 0 = normal.  Returns the previous setting.
+#ifdef SRPC_SX_PHASES
+extern "C" int srpc_debug_sx_phases(void* d_buf, uint64_t nblocks) {
+    unsigned long long* p = static_cast<unsigned long long*>(d_buf);
+    unsigned long long nb = nblocks;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(srpc_impl::g_sxph), &p, sizeof(p)) != hipSuccess) return SRPC_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(srpc_impl::g_sxph_blocks), &nb, sizeof(nb)) != hipSuccess) return SRPC_E_HIP;
+    return SRPC_OK;
+}
+#endif
+
+extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_tables(int mode) {
+    return static_cast<int>(srpc_impl::g_sx_mode.exchange(static_cast<uint32_t>(mode < 0 ? 0 : mode > 7 ? 7 : mode)));
+}

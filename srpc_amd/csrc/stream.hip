@@ -820,7 +820,7 @@ using namespace srpc_impl;
 
 extern "C" {
 
-int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out) {
+int srpc_legacy_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out) {
     if (!p || !out || !p->has_string) return SRPC_E_INVALID;
     uint64_t var = 0;
     if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
@@ -829,14 +829,14 @@ int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t 
     return SRPC_OK;
 }
 
-int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
-                               uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
-                               srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+int srpc_legacy_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                                  uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                                  srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
     if (!p || !p->has_string || !rec_offs || !scratch) return SRPC_E_INVALID;
     if (wire_len && !wire) return SRPC_E_INVALID;
     if (!aligned(rec_offs, 8) || !aligned(scratch, 256)) return SRPC_E_ALIGN;
     uint64_t need = 0, var = 0;
-    if (int rc = srpc_plan_var_stream_scratch_bytes(p, n, wire_len, &need)) return rc;
+    if (int rc = srpc_legacy_var_stream_scratch_bytes(p, n, wire_len, &need)) return rc;
     if (scratch_bytes < need) return SRPC_E_CAPACITY;
     srpc_plan_var_scratch_bytes(p, n, wire_len, &var);
     auto s = static_cast<hipStream_t>(stream);
@@ -860,7 +860,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     const uint64_t g = (C + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     const TimedCall timed;
-    const uint32_t mode = g_force_single.load(std::memory_order_relaxed);
+    uint32_t mode = g_force_single.load(std::memory_order_relaxed);
+    if (mode == 7) mode = 0;
     void* s1 = base + r256(L.total);
     if (mode == 2 && stream1_decodes(p)) {
         // the bounded single pass on its own
@@ -942,5 +943,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
 // the bounded one when it gives up; 6 = as 0 with the chunk pipeline's
 // hand-over forced.  Returns the previous setting.
 extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_force_single(int on) {
-    return static_cast<int>(srpc_impl::g_force_single.exchange(static_cast<uint32_t>(on < 0 ? 0 : on > 6 ? 6 : on)));
+    return static_cast<int>(srpc_impl::g_force_single.exchange(static_cast<uint32_t>(on < 0 ? 0 : on > 7 ? 7 : on)));
 }
+// Nonzero: srpc_gpu_unpack_var_stream runs these decoders (mode 7 = their
+// default order, 1..6 as above); 0 = the table-scan decoder of sdx.hip.
+extern "C" int srpc_legacy_stream_mode() { return static_cast<int>(srpc_impl::g_force_single.load()); }

@@ -1803,14 +1803,21 @@ __device__ __forceinline__ uint32_t parse_record_lds(const VarArgs& a, const uin
 // that is not exact (or whose base would leave the chars buffer) sets *bad;
 // then the general kernel (kOpt = false, gated on *bad) decodes the whole
 // batch again with the look-back and rewrites every output.
+// table (kOpt = false, several string fields): the caller's tile table
+// (srpc_gpu_var_tile_table: chars of each string field before every 256-record
+// tile) gives each tile its output bases instead of the look-back; each tile
+// checks its own totals against the table's differences (and table[0] = 0,
+// bases inside the chars buffers), so a wrong table is caught: *bad is set and
+// the look-back pass (gated on *bad) decodes the batch again.
 template <bool kOpt>
 __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, const uint8_t* __restrict__ wire,
                                                           uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
                                                           uint64_t n, uint64_t* __restrict__ look,
                                                           uint64_t* __restrict__ look2, uint32_t* __restrict__ ticket,
-                                                          srpc_unpack_status* st, uint32_t* __restrict__ bad) {
+                                                          srpc_unpack_status* st, uint32_t* __restrict__ bad,
+                                                          const uint64_t* __restrict__ table) {
     if constexpr (!kOpt)
-        if (bad && *bad == 0) return;  // the optimistic pass was exact everywhere
+        if (!table && bad && *bad == 0) return;  // the optimistic pass was exact everywhere
     PHASE_BEGIN
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint64_t s_tile, s_lo, s_hi, s_src, s_first;
@@ -1917,7 +1924,22 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         len_l[si * kBlock + i] = x;
         if (i == 0) {
             s_tot[si] = tot;
-            if (!kOpt) look_store(look + t * ns + si, (t == 0 ? kLookIncl : kLookAgg) | (tot & kLookVal));
+            if (!kOpt && !table) look_store(look + t * ns + si, (t == 0 ? kLookIncl : kLookAgg) | (tot & kLookVal));
+        }
+    }
+    if (!kOpt && table) {  // the tile's bases from the caller's table, checked
+        if (i == 0) s_inexact = 0;
+        __syncthreads();
+        if (i < ns) {
+            const uint64_t lo = table[t * ns + i], hi = table[(t + 1) * ns + i];
+            const bool ok = (t > 0 || lo == 0) && hi >= lo && hi - lo == s_tot[i] && hi <= wire_len;
+            s_pre[i] = lo;
+            if (!ok) s_inexact = 1;
+        }
+        __syncthreads();
+        if (s_inexact) {
+            if (i == 0) atomicOr(bad, 1u);
+            return;  // the look-back pass rewrites the batch
         }
     }
     if (kOpt) {  // the tile's chars base, valid when every record before it is exact
@@ -1988,7 +2010,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     };
     // string field si's look-back runs on wave si mod 4: the fields' round
     // trips overlap instead of adding up (two strings: one wave each)
-    if (!kOpt && (i >> 6) < ns) {
+    if (!kOpt && !table && (i >> 6) < ns) {
         bool stalled = false;
         for (uint32_t si = i >> 6; si < ns; si += kBlock / 64) {
 #if SRPC_RTU_NOLOOK  // A/B timing only: wrong offsets
@@ -2003,7 +2025,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
 #if SRPC_RTU_OFFLOAD
     // the waves that do not look back build every record's chars (the
     // look-back waves' records too), so the look-back is off the build's path
-    if (!kOpt && ns < kBlock / 64) {
+    if (!kOpt && !table && ns < kBlock / 64) {
         const uint32_t w = i >> 6, nb = kBlock - 64 * ns;
         if (w >= ns && fits) {
             for (uint32_t j = i - 64 * ns; j < nr; j += nb) {
@@ -2092,6 +2114,22 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     PHASE(5);
     PHASE_COUNT(6);
     PHASE_END
+}
+
+// The tile table of a batch from its string offsets: entry t * ns + s = chars
+// of string ordinal s before record min(256 t, n).
+struct TileTableArgs {
+    const uint64_t* soff[kMaxFields];
+    uint32_t ns;
+};
+__global__ void k_tile_table(TileTableArgs t, uint64_t n, uint64_t* __restrict__ table, uint64_t entries) {
+    for (uint64_t e = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < entries;
+         e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        const uint64_t tile = e / t.ns;
+        const uint32_t si = static_cast<uint32_t>(e % t.ns);
+        const uint64_t* so = t.soff[si];
+        table[e] = so[min<uint64_t>(tile * kBlock, n)] - so[0];
+    }
 }
 
 __global__ void k_str_offs_zero(VarArgs a) {  // n == 0: str_offs[f][0] = 0
@@ -2401,9 +2439,10 @@ int srpc_gpu_pack_var(const srpc_plan* p, const void* const* cols, const uint64_
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
-int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
-                        const uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
-                        srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                              const uint64_t* rec_offs, const uint64_t* table, void* const* cols,
+                              uint64_t* const* str_offs, srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes,
+                              void* stream) {
     const TimedCall timed;
     if (!p || !p->has_string) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
@@ -2461,11 +2500,21 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         const uint64_t w1 = grid * p->nstrings, w2 = ((grid + 63) / 64) * p->nstrings;
         const uint64_t words = 1 + w1 + w2;
         const uint32_t zgrid = static_cast<uint32_t>(std::min<uint64_t>((words + 255) / 256, 1024));
+        const uint64_t* no_table = nullptr;
         if (p->nstrings == 1) {
             hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st_done ? nullptr : st, bad, 1u);
             st_done = true;
             launch(k_unpack_var_rt<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
-                   wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad);
+                   wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad,
+                   no_table);
+            launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
+        } else if (table) {
+            // the tiles' bases from the caller's table; the look-back pass only
+            // when a tile's totals disagree with it
+            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st_done ? nullptr : st, bad, 1u);
+            st_done = true;
+            launch(k_unpack_var_rt<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
+                   wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad, table);
             launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
         } else {
             if (!reset_st()) return SRPC_E_HIP;
@@ -2473,7 +2522,7 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
         }
         launch(k_unpack_var_rt<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire, wire_len,
                rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st,
-               p->nstrings == 1 ? bad : nullptr);
+               p->nstrings == 1 || table ? bad : nullptr, no_table);
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     if (p->nstrings == 1 && n) {  // single-string fast path: no scan unless a record is not exact
@@ -2560,6 +2609,38 @@ int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_l
                static_cast<const uint64_t*>(nullptr), 0u, reinterpret_cast<const uint32_t*>(tiles),
                static_cast<const uint32_t*>(nullptr));
     }
+    return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
+
+int srpc_gpu_unpack_var(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
+                        const uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
+                        srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
+    return srpc_gpu_unpack_var_tiled(p, wire, wire_len, n, rec_offs, nullptr, cols, str_offs, st, scratch,
+                                     scratch_bytes, stream);
+}
+
+int srpc_var_tile_table_words(const srpc_plan* p, uint64_t n, uint64_t* out) {
+    if (!p || !out || !p->has_string) return SRPC_E_INVALID;
+    *out = ((n + kBlock - 1) / kBlock + 1) * p->nstrings;
+    return SRPC_OK;
+}
+
+int srpc_gpu_var_tile_table(const srpc_plan* p, const uint64_t* const* str_offs, uint64_t n, uint64_t* table,
+                            void* stream) {
+    const TimedCall timed;
+    if (!p || !p->has_string || !str_offs || !table) return SRPC_E_INVALID;
+    if (!aligned(table, 8)) return SRPC_E_ALIGN;
+    TileTableArgs t{};
+    uint32_t si = 0;
+    for (uint32_t f = 0; f < p->nfields; ++f) {
+        if (p->size[f]) continue;
+        if (!str_offs[f] || !aligned(str_offs[f], 8)) return SRPC_E_INVALID;
+        t.soff[si++] = str_offs[f];
+    }
+    t.ns = p->nstrings;
+    const uint64_t entries = ((n + kBlock - 1) / kBlock + 1) * t.ns;
+    launch(k_tile_table, dim3(static_cast<uint32_t>(std::min<uint64_t>((entries + 255) / 256, 4096))), dim3(256), 0,
+           static_cast<hipStream_t>(stream), t, n, table, entries);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 

@@ -242,6 +242,25 @@ class GpuPacker:
                                              _stream(stream)),
               "srpc_gpu_unpack_var")
 
+    def var_tile_table_words(self, n: int) -> int:
+        """u64 words of a batch's tile table (srpc_gpu_var_tile_table)."""
+        out = C.c_uint64()
+        check(_lib.lib().srpc_var_tile_table_words(self._h, n, C.byref(out)), "srpc_var_tile_table_words")
+        return out.value
+
+    def var_tile_table(self, str_offs: Sequence, n: int, table, stream=None) -> None:
+        """The tile table of n records from their string offsets (async)."""
+        check(_lib.lib().srpc_gpu_var_tile_table(self._h, self._str_offs(str_offs), n, _dptr(table), _stream(stream)),
+              "srpc_gpu_var_tile_table")
+
+    def unpack_var_tiled(self, wire, wire_len: int, n: int, rec_offs, table, cols: Sequence, str_offs: Sequence,
+                         scratch, scratch_bytes: int, status=None, stream=None) -> None:
+        """unpack_var with the batch's tile table (output bases without the look-back)."""
+        check(_lib.lib().srpc_gpu_unpack_var_tiled(self._h, _dptr(wire), wire_len, n, _dptr(rec_offs), _dptr(table),
+                                                   self._cols(cols), self._str_offs(str_offs), _dptr(status),
+                                                   _dptr(scratch), scratch_bytes, _stream(stream)),
+              "srpc_gpu_unpack_var_tiled")
+
     def var_stream_scratch_bytes(self, n: int, wire_len: int) -> int:
         """Device scratch for unpack_var_stream (256-byte aligned)."""
         out = C.c_uint64()

@@ -72,6 +72,9 @@ def main():
                     help="decoders (srpc_debug_stream_force_single, stream.hip): 0 default, 2 the bounded "
                          "pass alone, 3 chunk pipeline -> bounded pass, 4 the speculative pass never giving "
                          "up, 5 speculative pass -> bounded pass, 6 default with the hand-over forced")
+    ap.add_argument("--tables", type=int, default=0,
+                    help="srpc_debug_stream_tables bits (sdx.hip): 1 sF-only tables, 2 empty tables, "
+                         "4 the exact speculation filter")
     args = ap.parse_args()
 
     import numpy as np
@@ -86,6 +89,11 @@ def main():
         hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
         hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
         hook(args.single)
+    if args.tables:
+        import ctypes
+        th = srpc_amd._lib.lib().srpc_debug_stream_tables
+        th.argtypes, th.restype = [ctypes.c_int], ctypes.c_int
+        th(args.tables)
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream()
     rows = []
