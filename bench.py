@@ -95,7 +95,7 @@ def committed_profiles(dom_name: str, n: int) -> dict:
     return out
 
 
-def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 32, depth: int = 4) -> dict:
+def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int = 3) -> dict:
     """The host-terminated path (north_star: it "starts and ends in host
     memory", the socket buffers of the reference's transport.hpp:94-123), in
     both directions, pinned host buffers:

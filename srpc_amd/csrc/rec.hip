@@ -298,15 +298,21 @@ constexpr RecKernel make_rec(bool use_pack, bool use_unpack) {
 // B); TwoNumbers behind the add request (50-byte prefix), the subtract /
 // multiply requests (55) and a response (19).  A layout matches by prefix
 // length and field sizes, whatever the prefix bytes.
+#ifndef SRPC_REC_UK
+#define SRPC_REC_UK 2
+#endif
+#ifndef SRPC_REC_U
+#define SRPC_REC_U false
+#endif
 const RecKernel kRec[] = {
     // (pack, unpack): where each measured faster than the generic TILE kernels
     // (profiles/r03_paths_rec_ab.log; differences under ~0.02 of peak are noise)
     make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(true, true),   // 0.64 / 0.68 -> 0.80 / 0.72
-    make_rec<Lay<49, 4>, 4, 2>(false, false),
-    make_rec<Lay<15, 4>, 4, 4>(false, false),
-    make_rec<Lay<50, 4, 4>, 4, 2>(false, true),
-    make_rec<Lay<55, 4, 4>, 4, 2>(false, false),
-    make_rec<Lay<19, 4, 4>, 4, 4>(false, true),
+    make_rec<Lay<49, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
+    make_rec<Lay<15, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
+    make_rec<Lay<50, 4, 4>, 4, SRPC_REC_UK>(false, true),
+    make_rec<Lay<55, 4, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
+    make_rec<Lay<19, 4, 4>, 4, SRPC_REC_UK>(false, true),
 };
 constexpr int kNumRec = sizeof(kRec) / sizeof(kRec[0]);
 

@@ -62,6 +62,7 @@ static_assert(kSC % 16 == 0 && kSC <= 64, "16-byte window reads; a chunk's posit
 constexpr uint32_t kMargin = 2048;               // staged bytes past the block
 constexpr uint32_t kStage = kSB + kMargin + 32;  // + 16-byte alignment slack on both sides
 constexpr uint32_t kWin = 64;                    // entry window of a block's table (a lane per position)
+constexpr uint32_t kEnt = kWin + 1;              // table entries per block: the window's, then the extra slot
 constexpr uint32_t kGroup = 64;                  // blocks per group of the scan (a lane per block)
 constexpr int kMaxNC = 3;                        // chars values carried per state (string fields 0..ns-2)
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
@@ -126,6 +127,8 @@ struct SxArgs {
     uint32_t plaus;              // records that must parse from a candidate
     uint32_t cap;                // record starts a chunk can hold: 1 + kSC / fixed_bytes
     uint32_t nb, ng;             // blocks, groups
+    uint32_t gap[kMaxFields + 1];  // fixed bytes before string ordinal 0 (prefix included), between
+                                   // strings k - 1 and k, after the last string (the parse's program)
     uint32_t mode;               // test hooks: 1 = tables hold only the first speculated start, 2 = empty
                                  // tables, 4 = the exact filter at every position (A/B)
 };
@@ -263,59 +266,57 @@ struct StageOnlyRd {
 
 // orc_unpack's cursor over one record at p: the position after it, or p with
 // *err set (SRPC_STATUS_PREFIX / _BOUNDS); chars of string fields 0..NC-1
-// added to ch[].
+// added to ch[].  Every loop runs a uniform number of times with the error
+// as a predicate (no early exit): its counter stays wave-uniform, so the
+// schema words it indexes (a.gap[k]) are scalar loads -- an index made
+// divergent by an early return turns each of them into a vector load from
+// the kernel-argument segment, a memory round trip per field per parse.
 template <int NC, class Rd>
 __device__ __forceinline__ uint64_t parse_rd(const SxArgs& a, const Rd& r, uint64_t p, uint32_t* err,
                                              uint64_t (&ch)[kMaxNC + 1]) {
     const uint64_t W = a.W;
-    *err = 0;
+    uint32_t e = 0;
     if (a.prefix_len) {
         if (a.prefix_len > W - p) {
-            *err = SRPC_STATUS_BOUNDS;
-            return p;
+            e = SRPC_STATUS_BOUNDS;
+        } else {
+            uint64_t diff = 0;
+            uint32_t i = 0;
+            for (; i + 8 <= a.prefix_len; i += 8) diff |= r.u64(p + i) ^ r.pre64(i);
+            for (; i < a.prefix_len; ++i) diff |= r.u8(p + i) ^ r.pre8(i);
+            if (diff) e = SRPC_STATUS_PREFIX;
         }
-        uint32_t i = 0;
-        for (; i + 8 <= a.prefix_len; i += 8)
-            if (r.u64(p + i) != r.pre64(i)) {
-                *err = SRPC_STATUS_PREFIX;
-                return p;
-            }
-        for (; i < a.prefix_len; ++i)
-            if (r.u8(p + i) != r.pre8(i)) {
-                *err = SRPC_STATUS_PREFIX;
-                return p;
-            }
     }
-    uint64_t q = p + a.prefix_len;
+    // the fields as a program of runs: fixed bytes, then a string, ..., then
+    // the fixed bytes after the last string (a read past the wire anywhere in
+    // a run is the same BOUNDS error the field-by-field cursor meets there)
+    uint64_t q = p;
     uint64_t add[kMaxNC + 1] = {};
-    uint32_t si = 0;
-    for (uint32_t f = 0; f < a.nfields; ++f) {
-        const uint32_t sz = a.size[f];
-        if (sz) {
-            if (sz > W - q) {
-                *err = SRPC_STATUS_BOUNDS;
-                return p;
+    for (uint32_t k = 0; k < a.nstrings; ++k) {
+        const uint32_t g = a.gap[k] + 8;  // the fixed run and the string's u64 length
+        if (!e) {
+            if (g > W - q) {
+                e = SRPC_STATUS_BOUNDS;
+            } else {
+                q += g;
+                const uint64_t len = r.u64(q - 8);
+                if (len > W - q) {
+                    e = SRPC_STATUS_BOUNDS;
+                } else {
+                    q += len;
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) add[j] += k == static_cast<uint32_t>(j) ? len : 0;
+                }
             }
-            q += sz;
-            continue;
         }
-        if (8 > W - q) {
-            *err = SRPC_STATUS_BOUNDS;
-            return p;
-        }
-        const uint64_t len = r.u64(q);
-        q += 8;
-        if (len > W - q) {
-            *err = SRPC_STATUS_BOUNDS;
-            return p;
-        }
-        q += len;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) add[k] += si == static_cast<uint32_t>(k) ? len : 0;
-        ++si;
     }
+    const uint32_t gl = a.gap[a.nstrings];
+    if (!e && gl > W - q) e = SRPC_STATUS_BOUNDS;
+    *err = e;
+    if (e) return p;
+    q += gl;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) ch[k] += add[k];
+    for (int j = 0; j < NC; ++j) ch[j] += add[j];
     return q;
 }
 
@@ -468,11 +469,18 @@ __device__ __forceinline__ uint64_t chunk_mask_z(const SxArgs& a, const uint8_t*
     uint64_t mask = 0;
     const uint32_t k8 = a.prefix_len < 8 ? a.prefix_len : 8;
     const uint64_t pm = k8 == 8 ? ~0ull : (1ull << (8 * k8)) - 1;
+    const lds_u8c* sl = (lds_u8c*)st;
+    auto u64_at = [&](uint32_t off) -> uint64_t {
+        lds_u32c* q = reinterpret_cast<lds_u32c*>(sl + (off & ~3u));
+        const uint32_t s3 = off & 3, w0 = q[0], w1 = q[1], w2 = q[2];
+        return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, s3)) << 32) |
+               __builtin_amdgcn_alignbyte(w1, w0, s3);
+    };
     while (cand) {
         const uint32_t j = __builtin_ctzll(cand);
         cand &= cand - 1;
-        if (lds_u64(st, o + j) + j > lim0) continue;
-        if (a.prefix_len && ((lds_u64(st, at + j) ^ a.pre8) & pm)) continue;
+        if (u64_at(o + j) + j > lim0) continue;
+        if (a.prefix_len && ((u64_at(at + j) ^ a.pre8) & pm)) continue;
         mask |= 1ull << j;
     }
     return mask;
@@ -665,14 +673,14 @@ __device__ St<NC> walk_global(const SxArgs& a, const uint8_t* w, uint64_t x, uin
 }
 
 // Slot of position x in a block's table (header words h0 = window mask, h1 =
-// the first speculated start): its compact index, or -1 (a miss).
-__device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint32_t nslots, uint64_t b0, uint64_t x) {
-    if (h0) {
-        const uint64_t off = x - b0;
-        if (off < kWin && ((h0 >> off) & 1)) return __builtin_popcountll(h0 & ((1ull << off) - 1));
-        return -1;
-    }
-    return nslots && x == h1 ? 0 : -1;
+// the first speculated start, h3 = the first speculated start past the
+// window): its compact index (kWin for the extra slot), or -1 (a miss).
+__device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint64_t h3, uint32_t nslots, uint64_t b0,
+                                       uint64_t x) {
+    const uint64_t off = x - b0;
+    if (h0 && off < kWin) return ((h0 >> off) & 1) ? __builtin_popcountll(h0 & ((1ull << off) - 1)) : -1;
+    if (!h0 && nslots && x == h1) return 0;
+    return x == h3 ? static_cast<int>(kWin) : -1;
 }
 
 // Prologue shared by the speculation and the decode: the prefix and the
@@ -773,7 +781,9 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
 
     // speculation: chunk c = tid
     const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
-    uint64_t sp = ~0ull;  // the chunk's first plausible start
+    uint64_t sp = ~0ull;   // the chunk's first plausible start
+    uint64_t sq1 = ~0ull;  // the end of its first record, when the speculation parsed it
+    uint64_t sch1[kMaxNC + 1] = {};
     if (clo < b1) {
         if (clo == 0) {
             sp = 0;  // the stream starts at 0: no speculation
@@ -782,31 +792,65 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
             uint64_t mask = W < (1ull << 32) && !(a.mode & 4) ? chunk_mask_z(a, L.st, at, clo, chi)
                                                                : chunk_mask(a, L.st, at, clo, chi);
             const uint64_t passing = mask;
-            while (mask) {
-                const uint32_t j = __builtin_ctzll(mask);
-                if (plausible(a, so, clo + j)) {
-                    sp = clo + j;
-                    break;
-                }
-                mask &= mask - 1;
-            }
-            if (sp != ~0ull) {
-                // plausible candidates sp .. sp + 7 inside the chunk: the one
-                // with the smallest first string length (a start 1-3 bytes
-                // early reads the true length shifted up)
-                const uint32_t jb = static_cast<uint32_t>(sp - clo);
-                uint64_t cand = (passing >> (jb + 1)) & 0x7f;
-                uint64_t best = so.u64(sp + a.first_len_at), pick = sp;
-                while (cand) {
-                    const uint64_t q = sp + 1 + __builtin_ctzll(cand);
-                    cand &= cand - 1;
+            // the first cluster of passing positions (8 bytes from the first):
+            // its smallest first string length is the true start (a start
+            // 1-3 bytes early reads the true length shifted up), tested first
+            // -- one plausibility test per chunk on random data
+            if (mask) {
+                const uint32_t j0 = __builtin_ctzll(mask);
+                uint64_t cl = (mask >> j0) & 0xff;
+                uint64_t best = ~0ull, pick = ~0ull;
+                while (cl) {
+                    const uint64_t q = clo + j0 + __builtin_ctzll(cl);
+                    cl &= cl - 1;
                     const uint64_t l = so.u64(q + a.first_len_at);
-                    if (l < best && plausible(a, so, q)) {
+                    if (l < best) {
                         best = l;
                         pick = q;
                     }
                 }
-                sp = pick;
+                uint32_t err = SRPC_STATUS_BOUNDS;
+                uint64_t tmp[kMaxNC + 1] = {};
+                const uint64_t q1 = pick != ~0ull ? parse_rd<NC>(a, so, pick, &err, tmp) : 0;
+                bool ok = !err;
+                if (ok && a.plaus > 1 && q1 != W) {
+                    uint64_t t2[kMaxNC + 1];
+                    (void)parse_rd<0>(a, so, q1, &err, t2);
+                    ok = !err;
+                }
+                if (ok) {
+                    sp = pick;
+                    sq1 = q1;
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) sch1[k] = tmp[k];
+                }
+            }
+            if (sp == ~0ull) {
+                // otherwise: the first plausible position, then of the
+                // plausible ones within 8 bytes the smallest first length
+                while (mask) {
+                    const uint32_t j = __builtin_ctzll(mask);
+                    if (plausible(a, so, clo + j)) {
+                        sp = clo + j;
+                        break;
+                    }
+                    mask &= mask - 1;
+                }
+                if (sp != ~0ull) {
+                    const uint32_t jb = static_cast<uint32_t>(sp - clo);
+                    uint64_t cand = (passing >> (jb + 1)) & 0x7f;
+                    uint64_t best = so.u64(sp + a.first_len_at), pick = sp;
+                    while (cand) {
+                        const uint64_t q = sp + 1 + __builtin_ctzll(cand);
+                        cand &= cand - 1;
+                        const uint64_t l = so.u64(q + a.first_len_at);
+                        if (l < best && plausible(a, so, q)) {
+                            best = l;
+                            pick = q;
+                        }
+                    }
+                    sp = pick;
+                }
             }
         }
     }
@@ -814,7 +858,19 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     uint64_t cch[kMaxNC + 1] = {};
     uint32_t ccnt, cstop;
     uint64_t cexit;
-    walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+    if (sq1 != ~0ull) {  // the first record was parsed by the test above: walk on from its end
+#pragma unroll
+        for (int k = 0; k < NC; ++k) cch[k] = sch1[k];
+        walk_chunk<NC>(a, rd, sq1, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+        if (sq1 >= chi) {  // (the walk saw no record: cexit = ~0)
+            ccnt = 0;
+            cexit = sq1;
+            cstop = 0;
+        }
+        ++ccnt;
+    } else {
+        walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+    }
     Chunks<NC>& C = L.c;
     C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
     C.exit[tid] = cexit;
@@ -829,8 +885,21 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     // the table (wave 0, lane = window position): every plausible position of
     // the block's first kWin bytes; a window with none holds the first
     // speculated start (sF) alone.  The primary slot is sF's: the entry the
-    // speculation itself predicts.
-    if (tid >= 64) return;
+    // speculation itself predicts.  Wave 1 meanwhile adds the extra slot, the
+    // first speculated start past the window (a record longer than the window
+    // that ends where its chunk speculated: entered there, not walked).
+    if (tid >= 128) return;
+    if (tid >= 64) {
+        if (tid == 64) {
+            const uint32_t F2 = next_bit(C.has, kWin / kSC);
+            uint64_t sF2 = F2 < kBlock && b > 0 && !(a.mode & 3) ? b0 + C.start[F2] : ~0ull;
+            if (sF2 != ~0ull)
+                st_store<NC>(S.ent + (b * kEnt + kWin) * ew<NC>(),
+                             walk_chain<NC, false>(a, rd, C, b0, b1, sF2, nullptr, nullptr));
+            S.hdr[4 * b + 3] = sF2;
+        }
+        return;
+    }
     const uint32_t F = next_bit(C.has, 0);
     const uint64_t sF = F < kBlock ? b0 + C.start[F] : ~0ull;
     uint64_t mycand = ~0ull;
@@ -857,40 +926,104 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     if (mycand != ~0ull) {
         mine = walk_chain<NC, false>(a, rd, C, b0, b1, mycand, nullptr, nullptr);
         const uint32_t k = __builtin_popcountll(vmask & ((1ull << lane) - 1));
-        st_store<NC>(S.ent + (b * kWin + k) * ew<NC>(), mine);
+        st_store<NC>(S.ent + (b * kEnt + k) * ew<NC>(), mine);
     }
     if (lane == 0) {
+        // one segment from sF to the block's end (a single tail, leaving the
+        // block or stopping): a cursor entering at sF takes every chunk's
+        // records as speculated (k_sx_decode skips the chain walk)
+        uint32_t ntail = 0, lastc = 0;
+        for (int k = 0; k < 4; ++k) {
+            ntail += __builtin_popcountll(C.tail[k]);
+            if (C.tail[k]) lastc = 64 * k + 63 - __builtin_clzll(C.tail[k]);
+        }
+        const bool one = sF != ~0ull && ntail == 1 && (C.stop[lastc] || C.exit[lastc] >= b1);
         uint64_t* h = S.hdr + 4 * b;
         h[0] = wmask;
         h[1] = sF;
-        h[2] = nslots | (static_cast<uint64_t>(prim) << 8);
-        h[3] = 0;
+        h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull);
     }
     SXP(3);
 }
 
 // ---- phase 2: the scan of the tables ----------------------------------------------
-// A block's header and its first kKeep table entries, one block per lane.
+// A block's header and its first kKeep table entries, one block per lane;
+// and the runs of primary links: lane j's primary chain (from its block's
+// first speculated start h1) leaves the block exactly at block j + 1's, so a
+// cursor entering block j at its primary crosses blocks j .. run[j] by adding
+// the primary chains' records and chars (inclusive prefix sums over the lanes).
 template <int NC>
 struct Held {
-    uint64_t h0, h1;
+    uint64_t h0, h1, h3;
     uint32_t meta;  // slots | primary << 8
     uint64_t e[kKeep][ew<NC>()];
-    __device__ __forceinline__ void load(const SxScratch& S, uint64_t blk, bool ok) {
+    bool has_prim;
+    St<NC> pe;                          // the primary slot's chain
+    uint64_t icnt, ich[kMaxNC + 1];     // inclusive prefix over lanes of pe.cnt / pe.ch
+    uint32_t run;                       // the last block of the run of primary links from this one
+    __device__ __forceinline__ void load(const SxScratch& S, uint64_t blk, bool ok, uint32_t nbk) {
+        const uint32_t lane = threadIdx.x & 63;
         h0 = 0;
-        h1 = ~0ull;
+        h1 = h3 = ~0ull;
         meta = 0;
-        if (!ok) return;
-        const uint64_t* h = S.hdr + 4 * blk;
-        h0 = h[0];
-        h1 = h[1];
-        meta = static_cast<uint32_t>(h[2]);
-        const uint32_t ns = meta & 0xff;
+        has_prim = false;
+        pe = St<NC>{};
+        if (ok) {
+            const uint64_t* h = S.hdr + 4 * blk;
+            h0 = h[0];
+            h1 = h[1];
+            h3 = h[3];
+            meta = static_cast<uint32_t>(h[2]);
+            const uint32_t ns = meta & 0xff, prim = (meta >> 8) & 0xff;
 #pragma unroll
-        for (int k = 0; k < kKeep; ++k)
-            if (static_cast<uint32_t>(k) < ns)
+            for (int k = 0; k < kKeep; ++k)
+                if (static_cast<uint32_t>(k) < ns)
 #pragma unroll
-                for (uint32_t j = 0; j < ew<NC>(); ++j) e[k][j] = S.ent[(blk * kWin + k) * ew<NC>() + j];
+                    for (uint32_t j = 0; j < ew<NC>(); ++j) e[k][j] = S.ent[(blk * kEnt + k) * ew<NC>() + j];
+            if (prim != kNoPrim) {
+                has_prim = true;
+                pe = st_load<NC>(S.ent + (blk * kEnt + prim) * ew<NC>());
+            }
+        }
+        const uint64_t next_p = __shfl_down(h1, 1, 64);
+        const uint32_t next_has = __shfl_down(static_cast<uint32_t>(has_prim), 1, 64);
+        const bool link = has_prim && lane + 1 < nbk && next_has && !(pe.stop & 1) && pe.x == next_p;
+        const uint64_t lmask = __ballot(link);
+        const uint64_t rest = ~lmask & (~0ull << lane);
+        run = min<uint32_t>(rest ? __builtin_ctzll(rest) : 63, nbk ? nbk - 1 : 0);
+        icnt = has_prim ? pe.cnt : 0;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) ich[k] = has_prim ? pe.ch[k] : 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(icnt, d, 64);
+            if (lane >= static_cast<uint32_t>(d)) icnt += y;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const uint64_t z = __shfl_up(ich[k], d, 64);
+                if (lane >= static_cast<uint32_t>(d)) ich[k] += z;
+            }
+        }
+    }
+    // A cursor entering block j (a uniform lane) at its primary start crosses
+    // blocks j .. run[j] at once (per lane: `mine` says which lanes move).
+    __device__ __forceinline__ void jump(uint32_t j, St<NC>& s, bool mine) const {
+        if (!__ballot(mine)) return;
+        const uint32_t m = __builtin_amdgcn_readlane(run, j);
+        const uint64_t ex_cnt = rl64(icnt, j) - rl64(has_prim ? pe.cnt : 0, j);
+        const uint64_t in_cnt = rl64(icnt, m);
+        uint64_t dch[kMaxNC + 1];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) dch[k] = rl64(ich[k], m) - (rl64(ich[k], j) - rl64(has_prim ? pe.ch[k] : 0, j));
+        const uint64_t x = rl64(pe.x, m);
+        const uint32_t stp = __builtin_amdgcn_readlane(pe.stop, m);
+        if (mine) {
+            s.cnt += in_cnt - ex_cnt;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) s.ch[k] += dch[k];
+            s.x = x;
+            s.stop = stp;
+        }
     }
 };
 
@@ -902,7 +1035,7 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
                                               const Held<NC>& hv, uint32_t l, uint64_t blk, St<NC>& s, bool* miss,
                                               bool* off, uint8_t* stage, bool may_walk = true) {
     // the held words of lane l (uniform reads, every lane takes part)
-    const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l);
+    const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l), h3 = rl64(hv.h3, l);
     const uint32_t meta = __builtin_amdgcn_readlane(hv.meta, l);
     uint64_t e[kKeep][ew<NC>()];
 #pragma unroll
@@ -912,13 +1045,15 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
     const uint64_t b0 = blk * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
     // a block no record starts in (the cursor is past its end) passes the state on
     const bool act = !st_done(s, a.W) && s.x < b1;
-    const int idx = act ? slot_of(h0, h1, meta & 0xff, b0, s.x) : 0;
+    const int idx = act ? slot_of(h0, h1, h3, meta & 0xff, b0, s.x) : 0;
+    const bool walk = act && idx < 0 && may_walk;
+    // every lane of the wave takes part in the staging of walk_miss
+    St<NC> mw{};
+    if (__ballot(walk)) mw = walk_miss<NC>(a, w, stage, b0, b1, s.x, walk);
     if (act && idx < 0 && !may_walk) {  // a chain the caller gives up on instead of walking it
         s.stop = kDead;
         return;
     }
-    St<NC> mw{};
-    if (__ballot(act && idx < 0)) mw = walk_miss<NC>(a, w, stage, b0, b1, s.x, act && idx < 0);
     if (!act) return;
     St<NC> t;
     if (idx >= 0 && idx < kKeep) {
@@ -931,7 +1066,7 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
         }
         t = st_load<NC>(v);
     } else if (idx >= 0) {
-        t = st_load<NC>(S.ent + (blk * kWin + idx) * ew<NC>());
+        t = st_load<NC>(S.ent + (blk * kEnt + idx) * ew<NC>());
     } else {
         t = mw;
         *miss = true;
@@ -955,31 +1090,37 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     const uint64_t bf = g * kGroup;
     const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
     Held<NC> hv;
-    hv.load(S, bf + lane, lane < nbk);
+    hv.load(S, bf + lane, lane < nbk, nbk);
     const uint32_t ns0 = __builtin_amdgcn_readlane(hv.meta, 0) & 0xff;
     const bool act = lane < ns0;
     St<NC> s{};
     s.stop = 1;  // lanes past the slots stay put
-    if (act) s = st_load<NC>(S.ent + (bf * kWin + lane) * ew<NC>());
+    if (act) s = st_load<NC>(S.ent + (bf * kEnt + lane) * ew<NC>());
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     uint8_t* stage = stages[threadIdx.x >> 6];
     bool miss = false, off = false;
     const bool primary = lane == ((__builtin_amdgcn_readlane(hv.meta, 0) >> 8) & 0xff);
     for (uint32_t j = 1; j < nbk; ++j) {
+        // chains entering block j at its primary cross its whole run at once
+        const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
+        if (hp) hv.jump(j, s, act && !st_done(s, a.W) && s.x == rl64(hv.h1, j));
+        const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
+        if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
         St<NC> t = s;
         through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, primary);
         if (act) s = t;
     }
     if (act) st_store<NC>(S.gent + (g * kWin + lane) * ew<NC>(), s);
     // what the in-order pass over the groups reads first, in one record
-    uint64_t* q = S.gp + g * (3 + ew<NC>());
+    uint64_t* q = S.gp + g * (4 + ew<NC>());
     const uint32_t meta0 = __builtin_amdgcn_readlane(hv.meta, 0);
     if (lane == 0) {
         q[0] = rl64(hv.h0, 0);
         q[1] = rl64(hv.h1, 0);
         q[2] = meta0;
+        q[3] = rl64(hv.h3, 0);
     }
-    if (act && lane == ((meta0 >> 8) & 0xff)) st_store<NC>(q + 3, s);
+    if (act && lane == ((meta0 >> 8) & 0xff)) st_store<NC>(q + 4, s);
 }
 
 // One wave: the groups in order.  Each group's entry state (the cursor where
@@ -999,19 +1140,19 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
     bool miss = false, off = false;
     // lane l: group base + l -- its first block's header and the group's
     // primary entry (S.gp), the next batch's loaded while this one is walked
-    uint64_t nq[3 + E];
+    uint64_t nq[4 + E];
     auto fetch = [&](uint64_t base) {
         const uint64_t g = base + lane;
 #pragma unroll
-        for (uint32_t j = 0; j < 3 + E; ++j) nq[j] = g < a.ng ? S.gp[g * (3 + E) + j] : 0;
+        for (uint32_t j = 0; j < 4 + E; ++j) nq[j] = g < a.ng ? S.gp[g * (4 + E) + j] : 0;
     };
     fetch(0);
     for (uint64_t base = 0; base < a.ng; base += 64) {
         const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(64, a.ng - base));
         const uint64_t g = base + lane;
-        const uint64_t h0 = nq[0], h1 = nq[1];
+        const uint64_t h0 = nq[0], h1 = nq[1], h3 = nq[3];
         const uint32_t meta = static_cast<uint32_t>(nq[2]);
-        St<NC> pe = st_load<NC>(nq + 3);  // the group's chain from its primary slot (its first block's sF = h1)
+        St<NC> pe = st_load<NC>(nq + 4);  // the group's chain from its primary slot (its first block's sF = h1)
         fetch(base + 64);
         const bool has_prim = lane < cnt && ((meta >> 8) & 0xff) != kNoPrim;
         // link k -> k + 1: group k's primary chain enters group k + 1 at its primary
@@ -1037,7 +1178,7 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
         uint32_t l = 0;
         while (l < cnt) {
             const uint64_t gl = base + l;
-            const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l);
+            const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l), lh3 = rl64(h3, l);
             const uint32_t lmeta = __builtin_amdgcn_readlane(meta, l);
             const uint32_t lprim = (lmeta >> 8) & 0xff;
             if (!st_done(s, W) && lprim != kNoPrim && s.x == lh1) {
@@ -1083,8 +1224,8 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
             if (s.x >= min<uint64_t>(bend * kSB, W)) continue;  // the whole group lies inside one record
             const uint64_t blk = s.x / kSB;
             int idx = -1;
-            if (blk == bf) idx = slot_of(lh0, lh1, lmeta & 0xff, bf * kSB, s.x);
-            if (idx >= 0) {
+            if (blk == bf) idx = slot_of(lh0, lh1, lh3, lmeta & 0xff, bf * kSB, s.x);
+            if (idx >= 0 && idx < static_cast<int>(kWin)) {  // (no group-table entry for the extra slot)
                 const St<NC> e = st_load<NC>(S.gent + (gl * kWin + idx) * E);
                 if (e.stop != kDead) {  // (the primary slot's is taken above)
                     off = true;
@@ -1098,10 +1239,10 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
                 if (s.x >= b1) continue;
                 const uint64_t* h = S.hdr + 4 * j;
                 const uint64_t m = h[2];
-                const int k = slot_of(h[0], h[1], static_cast<uint32_t>(m & 0xff), b0, s.x);
+                const int k = slot_of(h[0], h[1], h[3], static_cast<uint32_t>(m & 0xff), b0, s.x);
                 if (k != static_cast<int>((m >> 8) & 0xff)) off = true;
                 if (k >= 0) {
-                    st_add<NC>(s, st_load<NC>(S.ent + (j * kWin + k) * E));
+                    st_add<NC>(s, st_load<NC>(S.ent + (j * kEnt + k) * E));
                 } else {
                     st_add<NC>(s, walk_miss<NC>(a, w, stage, b0, b1, s.x, true));
                     miss = true;
@@ -1163,18 +1304,42 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
     const uint64_t bf = g * kGroup;
     const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
     Held<NC> hv;
-    hv.load(S, bf + lane, lane < nbk);
+    hv.load(S, bf + lane, lane < nbk, nbk);
     St<NC> s = st_load<NC>(S.gin + g * E);
     uint64_t out[E];
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     uint8_t* stage = stages[threadIdx.x >> 6];
     bool miss = false, off = false;
-    for (uint32_t j = 0; j < nbk; ++j) {
+    for (uint32_t j = 0; j < nbk;) {
+        const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
+        if (hp && !st_done(s, a.W) && s.x == rl64(hv.h1, j)) {
+            // entering block j at its primary: blocks j .. run[j] in one step,
+            // each block k of the run entered at its primary with the records
+            // and chars of the run's blocks before it
+            const uint32_t m = __builtin_amdgcn_readlane(hv.run, j);
+            const uint64_t ex_cnt = rl64(hv.icnt, j) - rl64(hv.has_prim ? hv.pe.cnt : 0, j);
+            uint64_t ex_ch[kMaxNC + 1];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) ex_ch[k] = rl64(hv.ich[k], j) - rl64(hv.has_prim ? hv.pe.ch[k] : 0, j);
+            if (lane >= j && lane <= m) {
+                St<NC> v{};
+                v.x = hv.h1;
+                v.cnt = s.cnt + (hv.icnt - hv.pe.cnt) - ex_cnt;
+#pragma unroll
+                for (int k = 0; k < NC; ++k) v.ch[k] = s.ch[k] + (hv.ich[k] - hv.pe.ch[k]) - ex_ch[k];
+                v.stop = 0;
+                st_store<NC>(out, v);
+            }
+            hv.jump(j, s, true);
+            j = m + 1;
+            continue;
+        }
         uint64_t v[E];
         st_store<NC>(v, s);
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) out[k] = lane == j ? v[k] : out[k];
         through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage);
+        ++j;
     }
     if (lane < nbk)
 #pragma unroll
@@ -1230,6 +1395,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     // flight at once (a block no record of the batch starts in wastes its stage)
     SXP_BEGIN
     const St<NC> s = st_load<NC>(S.bst + b * E);
+    const uint64_t hsF = S.hdr[4 * b + 1], hmeta = S.hdr[4 * b + 2];
     const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
     const uint8_t sb = clo < b1 ? S.spec[b * kBlock + tid] : kNoSpec;
     const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);
@@ -1243,6 +1409,19 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     uint32_t ccnt, cstop;
     uint64_t cexit;
     walk_chunk<0>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, L.u.w.list + tid * kListCap);
+    uint32_t nrec;
+    if (((hmeta >> 16) & 1) && x == hsF) {
+        // entered at the first speculated start of a block whose chunks form
+        // one segment: every chunk's records, in order, are the block's
+        uint64_t tot;
+        const uint32_t fb = static_cast<uint32_t>(block_xscan(ccnt, &tot, L.ws));
+        for (uint32_t k = 0; k < ccnt; ++k)
+            L.tbl[fb + k] = static_cast<uint16_t>(tid * kSC + L.u.w.list[tid * kListCap + k]);
+        __syncthreads();
+        nrec = static_cast<uint32_t>(min<uint64_t>(tot, kMaxRec));
+        SXP(9);
+        SXP(10);
+    } else {
     C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
     C.exit[tid] = cexit;
     C.stop[tid] = static_cast<uint8_t>(cstop);
@@ -1293,7 +1472,8 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
         for (uint32_t k = 0; k < ccnt; ++k)
             L.tbl[fb + (e1 - e0) + k] = static_cast<uint16_t>(tid * kSC + L.u.w.list[tid * kListCap + k]);
     __syncthreads();
-    const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(tot, kMaxRec));
+    nrec = static_cast<uint32_t>(min<uint64_t>(tot, kMaxRec));
+    }
     SXP(11);
 
     // records r = R + k of the batch, up to index n (record n's start)
@@ -1472,11 +1652,11 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     L.hdr = o;
     o += r256(8 * 4 * L.nb);
     L.ent = o;
-    o += r256(8 * E * kWin * L.nb);
+    o += r256(8 * E * kEnt * L.nb);
     L.gent = o;
     o += r256(8 * E * kWin * L.ng);
     L.gp = o;
-    o += r256(8 * (3 + E) * L.ng);
+    o += r256(8 * (4 + E) * L.ng);
     L.gin = o;
     o += r256(8 * E * L.ng);
     L.bst = o;
@@ -1585,6 +1765,18 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     a.plaus = p->prefix_len >= 8 ? kPlausPrefixed : kPlausBare;
     for (uint32_t i = 0; i < 8 && i < p->prefix_len; ++i) a.pre8 |= static_cast<uint64_t>(p->h_prefix[i]) << (8 * i);
     a.cap = 1 + kSC / p->fixed_bytes;
+    {
+        uint32_t k = 0, run = p->prefix_len;
+        for (uint32_t f = 0; f < p->nfields; ++f) {
+            if (p->size[f]) {
+                run += p->size[f];
+                continue;
+            }
+            a.gap[k++] = run;
+            run = 0;
+        }
+        a.gap[k] = run;
+    }
     a.nb = static_cast<uint32_t>(SL.nb);
     a.ng = static_cast<uint32_t>(SL.ng);
     a.mode = g_sx_mode.load(std::memory_order_relaxed);
