@@ -298,21 +298,19 @@ constexpr RecKernel make_rec(bool use_pack, bool use_unpack) {
 // B); TwoNumbers behind the add request (50-byte prefix), the subtract /
 // multiply requests (55) and a response (19).  A layout matches by prefix
 // length and field sizes, whatever the prefix bytes.
-#ifndef SRPC_REC_UK
-#define SRPC_REC_UK 2
-#endif
-#ifndef SRPC_REC_U
-#define SRPC_REC_U false
-#endif
 const RecKernel kRec[] = {
     // (pack, unpack): where each measured faster than the generic TILE kernels
-    // (profiles/r03_paths_rec_ab.log; differences under ~0.02 of peak are noise)
-    make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(true, true),   // 0.64 / 0.68 -> 0.80 / 0.72
-    make_rec<Lay<49, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
-    make_rec<Lay<15, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
-    make_rec<Lay<50, 4, 4>, 4, SRPC_REC_UK>(false, true),
-    make_rec<Lay<55, 4, 4>, 4, SRPC_REC_UK>(false, SRPC_REC_U),
-    make_rec<Lay<19, 4, 4>, 4, SRPC_REC_UK>(false, true),
+    // (profiles/r03_paths_rec_ab.log, profiles/r04_rec_unpack_ab.log;
+    // differences under ~0.02 of peak are noise).  Tile depth K: the records
+    // behind an envelope unpack best one round per wave (K = 1: a 53-63 byte
+    // record's tile is ~14 KiB of LDS, ~11 waves per CU instead of ~5 at K =
+    // 2), the short responses at K = 2.
+    make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(true, true),  // 0.64 / 0.68 -> 0.80 / 0.72
+    make_rec<Lay<49, 4>, 4, 1>(false, true),                // unpack 0.76 -> 0.77
+    make_rec<Lay<15, 4>, 4, 2>(false, true),                // 0.74 -> 0.77
+    make_rec<Lay<50, 4, 4>, 4, 1>(false, true),             // 0.72 (K = 2) -> 0.76
+    make_rec<Lay<55, 4, 4>, 4, 1>(false, true),             // 0.69 -> 0.78
+    make_rec<Lay<19, 4, 4>, 4, 2>(false, true),             // 0.76 (K = 4) -> 0.78
 };
 constexpr int kNumRec = sizeof(kRec) / sizeof(kRec[0]);
 

@@ -42,6 +42,7 @@ def main():
              ("two_str_request_0-32_4M", [S, I32, S], 1 << 22, lambda k, n, r: gen_random(k, n, r, 32),
               srpc_amd.request_prefix("Svc_servicer::method", "TwoStr")),
              ("string_0-16_8M", [S], 1 << 23, lambda k, n, r: gen_random(k, n, r, 16), b""),
+             ("string_0-1024_1M", [S], 1 << 20, lambda k, n, r: gen_random(k, n, r, 1024), b""),
              ("zh4_zero_heavy_4M", [I8, S, oracle.INT16, S], 1 << 22, gen_zero_heavy, b"")]
     for name, kinds, n, gen, prefix in cases:
         if args.only not in name:
