@@ -265,6 +265,214 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
     return false;
 }
 
+// ---- layouts known at compile time -------------------------------------------
+// The staged kernels below move each field between the two LDS images at
+// offsets known only at run time (byte-wide LDS traffic, ~55% bank conflicts
+// on the all-kinds struct: profiles/r04_pmc_aos.txt).  For the struct layouts
+// the benchmarks and the reference's examples use, the layout is a template
+// instead (as rec.hip does for columns): a lane holds G structs in registers
+// (16-byte loads straight from HBM; the wave's loads cover whole lines), builds
+// its G wire records as dwords with byte permutes fixed at compile time, and
+// the wave streams its wire tile through LDS in coalesced 16-byte pieces (an
+// odd dword stride per lane: no bank conflicts).  Unpack is the mirror; bytes
+// of a struct no field covers come from the fill record (fresh objects) or
+// from the struct itself (in place: the lane reads it first).
+struct AosLayAllKindsV {  // {vtable*, bool, int8, char, int16, int32, int64}: 32 bytes
+    static constexpr int RS = 32, NF = 6;
+    static constexpr int ROFF[NF] = {8, 9, 10, 12, 16, 24}, SZ[NF] = {1, 1, 1, 2, 4, 8};
+};
+struct AosLayAllKinds {  // the same without the vtable slot: 24 bytes
+    static constexpr int RS = 24, NF = 6;
+    static constexpr int ROFF[NF] = {0, 1, 2, 4, 8, 16}, SZ[NF] = {1, 1, 1, 2, 4, 8};
+};
+
+template <class L>
+struct AosT {
+    static constexpr int WS = [] {
+        int w = 0;
+        for (int f = 0; f < L::NF; ++f) w += L::SZ[f];
+        return w;
+    }();
+    static constexpr int woff(int f) {
+        int o = 0;
+        for (int i = 0; i < f; ++i) o += L::SZ[i];
+        return o;
+    }
+    static constexpr int wfield(int b) {  // field of wire byte b
+        int o = 0;
+        for (int i = 0; i < L::NF; ++i) {
+            if (b < o + L::SZ[i]) return i;
+            o += L::SZ[i];
+        }
+        return L::NF - 1;
+    }
+    static constexpr int rfield(int b) {  // field of struct byte b, or -1
+        for (int i = 0; i < L::NF; ++i)
+            if (b >= L::ROFF[i] && b < L::ROFF[i] + L::SZ[i]) return i;
+        return -1;
+    }
+    static constexpr bool dword_used(int d) {  // dword d of a lane's structs holds a field byte
+        for (int b = 4 * d; b < 4 * d + 4; ++b)
+            if (rfield(b % L::RS) >= 0) return true;
+        return false;
+    }
+    static constexpr bool piece_used(int q) {  // 16-byte piece q of a lane's structs holds a field byte
+        return dword_used(4 * q) || dword_used(4 * q + 1) || dword_used(4 * q + 2) || dword_used(4 * q + 3);
+    }
+};
+
+__device__ __forceinline__ uint32_t aos_byte(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+
+constexpr int kAosLayG = 4;  // structs per lane
+constexpr int kAosWave = 64;
+
+template <class L>
+__global__ __launch_bounds__(kAosWave, 8) void k_pack_aos_lay(const uint8_t* __restrict__ recs, uint8_t* __restrict__ wire,
+                                                          uint64_t n) {
+    using T = AosT<L>;
+    constexpr int G = kAosLayG, SD = G * L::RS / 4, WD = G * T::WS / 4, TR = kAosWave * G;
+    static_assert((G * L::RS) % 16 == 0 && L::RS % 4 == 0 && (G * T::WS) % 4 == 0,
+                  "16-byte pieces of a lane's structs, whole wire dwords per lane");
+    __shared__ __attribute__((aligned(16))) uint32_t img[kAosWave * WD + 4];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * TR + lane * G;  // the lane's first struct
+    uint32_t sd[SD] = {};
+    if (r0 + G <= n) {  // the lane's structs in 16-byte pieces (those holding a field byte)
+        const v4u* src = reinterpret_cast<const v4u*>(recs + r0 * L::RS);
+#pragma unroll
+        for (int q = 0; q < SD / 4; ++q) {
+            if (!T::piece_used(q)) continue;
+            const v4u v = src[q];  // plain: the wave's strided pieces share lines (non-temporal ones refetch them)
+            sd[4 * q] = v.x;
+            sd[4 * q + 1] = v.y;
+            sd[4 * q + 2] = v.z;
+            sd[4 * q + 3] = v.w;
+        }
+    } else {  // the array's last lane: its structs below n, a dword at a time
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(recs + r0 * L::RS);
+#pragma unroll
+        for (int d = 0; d < SD; ++d)
+            if (T::dword_used(d) && r0 + (4 * d) / L::RS < n) sd[d] = src[d];
+    }
+#pragma unroll
+    for (int d = 0; d < WD; ++d) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 4 * d + i, r = j / T::WS, b = j % T::WS, f = T::wfield(b);
+            v |= aos_byte(sd, r * L::RS + L::ROFF[f] + (b - T::woff(f))) << (8 * i);
+        }
+        img[lane * WD + d] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes before its reads
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * TR;
+    const uint64_t nr = min<uint64_t>(TR, n - t0);
+    const uint32_t bytes = static_cast<uint32_t>(nr) * T::WS, full = bytes >> 4;
+    uint8_t* dst = wire + t0 * T::WS;
+    for (uint32_t c = lane; c < full; c += kAosWave) {
+        const v4u v = reinterpret_cast<const v4u*>(img)[c];
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst) + c);
+    }
+    for (uint32_t i = 16 * full + lane; i < bytes; i += kAosWave) dst[i] = reinterpret_cast<const uint8_t*>(img)[i];
+}
+
+template <class L, bool kFill>
+__global__ __launch_bounds__(kAosWave) void k_unpack_aos_lay(const uint8_t* __restrict__ wire, uint8_t* __restrict__ recs,
+                                                            uint64_t n, AosArgs a) {
+    using T = AosT<L>;
+    constexpr int G = kAosLayG, SD = G * L::RS / 4, WD = G * T::WS / 4, TR = kAosWave * G;
+    __shared__ __attribute__((aligned(16))) uint32_t img[kAosWave * WD + 4];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * TR;
+    const uint64_t nr = min<uint64_t>(TR, n - t0);
+    const uint32_t bytes = static_cast<uint32_t>(nr) * T::WS, full = bytes >> 4;
+    const uint8_t* src = wire + t0 * T::WS;
+    for (uint32_t c = lane; c < full; c += kAosWave)
+        reinterpret_cast<v4u*>(img)[c] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + c);
+    for (uint32_t i = 16 * full + lane; i < bytes; i += kAosWave) reinterpret_cast<uint8_t*>(img)[i] = src[i];
+    const uint64_t r0 = t0 + lane * G;
+    v4u* out = reinterpret_cast<v4u*>(recs + r0 * L::RS);
+    // in place: the lane's structs as they are (the bytes no field covers stay)
+    const bool whole = r0 + G <= n;
+    uint32_t old[SD] = {};
+    if constexpr (!kFill) {
+        if (whole) {
+#pragma unroll
+            for (int q = 0; q < SD / 4; ++q) {
+                const v4u v = out[q];
+                old[4 * q] = v.x;
+                old[4 * q + 1] = v.y;
+                old[4 * q + 2] = v.z;
+                old[4 * q + 3] = v.w;
+            }
+        } else {
+            const uint32_t* o32 = reinterpret_cast<const uint32_t*>(out);
+#pragma unroll
+            for (int d = 0; d < SD; ++d)
+                if (r0 + (4 * d) / L::RS < n) old[d] = o32[d];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    uint32_t w[WD];
+#pragma unroll
+    for (int d = 0; d < WD; ++d) w[d] = img[lane * WD + d];
+    uint32_t o[SD];
+#pragma unroll
+    for (int d = 0; d < SD; ++d) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sb = 4 * d + i, r = sb / L::RS, ob = sb % L::RS, f = T::rfield(ob);
+            uint32_t byte;
+            if (f >= 0) byte = aos_byte(w, r * T::WS + T::woff(f) + (ob - L::ROFF[f]));
+            else if (kFill) byte = (a.fillw[ob >> 2] >> (8 * (ob & 3))) & 0xffu;
+            else byte = aos_byte(old, sb);
+            v |= byte << (8 * i);
+        }
+        o[d] = v;
+    }
+    if (whole) {
+        // plain stores: the L2 merges the wave's strided pieces into whole lines
+#pragma unroll
+        for (int q = 0; q < SD / 4; ++q) out[q] = v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+    } else {
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+#pragma unroll
+        for (int d = 0; d < SD; ++d)
+            if (r0 + (4 * d) / L::RS < n) o32[d] = o[d];
+    }
+}
+
+template <class L>
+bool aos_lay_match(const AosArgs& a) {
+    if (a.prefix_len || a.rstride != static_cast<uint32_t>(L::RS) || a.nfields != static_cast<uint32_t>(L::NF)) return false;
+    for (int f = 0; f < L::NF; ++f)
+        if (a.roff[f] != static_cast<uint32_t>(L::ROFF[f]) || a.size[f] != static_cast<uint32_t>(L::SZ[f])) return false;
+    return true;
+}
+
+// The layout kernels for a struct array that matches one (16-byte aligned
+// array and wire), else false.
+template <class L>
+bool launch_aos_lay1(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+    if (!aos_lay_match<L>(a)) return false;
+    const uint64_t g = (n + kAosWave * kAosLayG - 1) / (kAosWave * kAosLayG);
+    if (g > 0x7fffffffull) return false;
+    const dim3 grid(static_cast<uint32_t>(g));
+    if (pack) launch(k_pack_aos_lay<L>, grid, dim3(kAosWave), 0, s, src, dst, n);
+    else if (a.fill) launch(k_unpack_aos_lay<L, true>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
+    else launch(k_unpack_aos_lay<L, false>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
+    return true;
+}
+
+bool launch_aos_lay(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+    if (!aligned(src, 16) || !aligned(dst, 16)) return false;
+    return launch_aos_lay1<AosLayAllKindsV>(a, pack, src, dst, n, s) ||
+           launch_aos_lay1<AosLayAllKinds>(a, pack, src, dst, n, s);
+}
+
 // HBM bytes [0, bytes) of a tile -> LDS (16-byte pieces, then single bytes).
 __device__ __forceinline__ void tile_in(uint8_t* lds, const uint8_t* __restrict__ g, uint32_t bytes) {
     const uint32_t full = bytes >> 4;
@@ -401,9 +609,15 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos_staged(AosArgs a, const u
 // Staged-kernel tiling: R (a multiple of 16) records whose two images fill
 // about kAosTileBytes of LDS; returns the LDS bytes, sets a->R / a->simg.
 constexpr uint32_t kAosTileBytes = 24 * 1024;
+// A/B knob (SRPC_AOS_TILE_BYTES at load): the two images' budget
+const uint32_t g_aos_tile_bytes = [] {
+    const char* e = std::getenv("SRPC_AOS_TILE_BYTES");
+    const long v = e ? std::atol(e) : 0;
+    return v >= 1024 && v <= 64 * 1024 ? static_cast<uint32_t>(v) : kAosTileBytes;
+}();
 uint32_t staged_tiling(AosArgs* a) {
     const uint32_t per = a->ident ? a->wstride : a->wstride + a->rstride;
-    uint32_t R = std::max<uint32_t>(16, (kAosTileBytes / per) & ~15u);
+    uint32_t R = std::max<uint32_t>(16, (g_aos_tile_bytes / per) & ~15u);
     a->R = R;
     const uint32_t wimg = (R * a->wstride + 15) & ~15u;
     a->simg = a->ident ? 0 : wimg;
@@ -470,6 +684,12 @@ const bool g_aos_unstaged = [] {
     return e && e[0] == '1';
 }();
 
+// A/B switch (SRPC_AOS_NOLAY=1 at load): the staged kernels for the layouts above too.
+const bool g_aos_nolay = [] {
+    const char* e = std::getenv("SRPC_AOS_NOLAY");
+    return e && e[0] == '1';
+}();
+
 }  // namespace
 }  // namespace srpc_impl
 
@@ -488,6 +708,9 @@ int srpc_gpu_pack_aos(const srpc_plan* p, const void* d_records, uint64_t record
     if (!aligned(d_wire, 16)) return SRPC_E_ALIGN;
     if (!a.ident && !g_aos_unstaged &&
         launch_aos_run(a, true, static_cast<const uint8_t*>(d_records), d_wire, n, static_cast<hipStream_t>(stream)))
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    if (!g_aos_unstaged && !g_aos_nolay &&
+        launch_aos_lay(a, true, static_cast<const uint8_t*>(d_records), d_wire, n, static_cast<hipStream_t>(stream)))
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     if (aligned(d_records, 16) && !g_aos_unstaged) {
         const uint32_t lds = staged_tiling(&a);
@@ -531,6 +754,9 @@ static int unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_l
     }
     if (n_fit && !a.ident && !g_aos_unstaged && !(a.fill && g_aos_fill_staged) &&
         launch_aos_run(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
+        return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
+    if (n_fit && !g_aos_unstaged && !g_aos_nolay &&
+        launch_aos_lay(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
     if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
         const uint32_t lds = staged_tiling(&a);

@@ -2,8 +2,8 @@
 // offsets out[0..n], out[n] = the total: per 2048 values a block total
 // (xscan_reduce), one workgroup scanning the block totals in place
 // (xscan_partials), then the apply pass (xscan_apply).  Used for the
-// response offsets of a frame batch (frames.hip) and the record numbers of a
-// stream's chunks (stream.hip).  Scratch: xscan_parts(n) u64 words.
+// response offsets of a frame batch (frames.hip).  Scratch: xscan_parts(n)
+// u64 words.
 #pragma once
 
 #include <hip/hip_runtime.h>

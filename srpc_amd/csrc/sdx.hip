@@ -6,7 +6,7 @@
 // unpack sharing the buffer as in tests/packer_test.cpp:77-88), so where a
 // record starts is known only once every record before it was read.  Here:
 //
-// 1. k_sx_spec, a workgroup per 8 KiB block of the wire (+ a 2 KiB margin),
+// 1. k_sx_spec, a workgroup per 8 KiB block of the wire (+ a 1.5 KiB margin),
 //    staged in LDS by LDS-DMA.  A lane per 32-byte chunk speculates the
 //    chunk's first record start (a filter over its 32 positions from register
 //    windows of the stage, then whole records must parse; of the plausible
@@ -35,8 +35,9 @@
 // 3. k_sx_decode, a workgroup per block: the block again (its speculated
 //    chunk starts from scratch, the chunks walked again from LDS), the chain
 //    from the block's exact entry (whole segments jumped), and the block's
-//    records written: rec_offs, fixed columns, str_offs, chars through an LDS
-//    image leaving in aligned 16-byte stores.  Each block's output bases come
+//    records written: rec_offs, fixed columns, str_offs, and the chars (a
+//    lane per record, straight from the stage: aligned 16-byte stores between
+//    byte / dword edges; a string of 8 KiB or more by the whole block).  Each block's output bases come
 //    from phase 2: no look-back, no wait.
 //
 // Error semantics are orc_unpack's (oracle/packer_oracle.c): the first record
@@ -59,21 +60,22 @@ namespace {
 constexpr uint32_t kSB = 8192;                   // wire bytes per block (one workgroup)
 constexpr uint32_t kSC = kSB / kBlock;           // 32: wire bytes per speculating lane
 static_assert(kSC % 16 == 0 && kSC <= 64, "16-byte window reads; a chunk's positions fit one 64-bit mask");
-constexpr uint32_t kMargin = 2048;               // staged bytes past the block
+constexpr uint32_t kMargin = 1536;               // staged bytes past the block
 constexpr uint32_t kStage = kSB + kMargin + 32;  // + 16-byte alignment slack on both sides
 constexpr uint32_t kWin = 64;                    // entry window of a block's table (a lane per position)
 constexpr uint32_t kEnt = kWin + 1;              // table entries per block: the window's, then the extra slot
 constexpr uint32_t kGroup = 64;                  // blocks per group of the scan (a lane per block)
 constexpr int kMaxNC = 3;                        // chars values carried per state (string fields 0..ns-2)
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
-constexpr uint32_t kImage = kSB + kMargin + 64;  // chars image of one string field
+constexpr uint32_t kHugeLog2 = 13;               // strings from 8 KiB: copied by the whole block
+constexpr uint16_t kFar = 0xFFFF;
 constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint16_t kNoStart = 0xFFFF;
 constexpr uint8_t kNoSpec = 0xFF;
 constexpr int kKeep = 4;                         // table entries per block the scans hold in registers
 constexpr uint64_t kCnt40 = (1ull << 40) - 1;
 constexpr uint32_t kNoPrim = 0xFF;
-constexpr uint32_t kListCap = 5;                 // record starts a 32-byte chunk holds (records >= 8 bytes)
+constexpr uint32_t kListCap = 4;                 // record starts a 32-byte chunk holds (records >= 8 bytes apart)
 constexpr uint32_t kDead = 0x81;                 // stop bits of a group-table chain given up (k_sx_groups)
 
 // control words (scratch; k_sx_spec block 0 zeroes them each call)
@@ -142,6 +144,7 @@ struct SxScratch {
     uint64_t* gin;   // per group: the cursor's state where the group starts (E words)
     uint64_t* bst;   // per block: the cursor's state where the block starts (E words)
     uint64_t* ctl;   // kCtlWords
+    uint16_t* rl;    // per block, kMaxRec slots: its chunks' record starts in order (offsets from the block)
 };
 
 // A chain's result / the cursor's state: position (exit, or the next record
@@ -256,7 +259,7 @@ struct StagedRd {
 // len * 256 + a char would otherwise send lanes to global memory.
 struct StageOnlyRd {
     StagedRd s;
-    __device__ __forceinline__ uint64_t u64(uint64_t p) const { return p >= s.lo && p + 8 <= s.hi ? s.u64(p) : ~0ull; }
+    __device__ __forceinline__ uint64_t u64(uint64_t p) const { return p >= s.lo && p + 8 <= s.hi ? s.u64_lds(p) : ~0ull; }
     __device__ __forceinline__ uint8_t u8(uint64_t p) const {
         return p >= s.lo && p < s.hi ? s.lds[p - s.base] : static_cast<uint8_t>(~s.pre[0]);
     }
@@ -446,9 +449,10 @@ __device__ __forceinline__ uint64_t chunk_mask(const SxArgs& a, const uint8_t* s
 // per position), and each candidate is then tested exactly (its length, the
 // prefix's first 8 bytes) from LDS.  The same mask as chunk_mask.
 __device__ __forceinline__ uint64_t chunk_mask_z(const SxArgs& a, const uint8_t* st, uint32_t at, uint64_t clo,
-                                                 uint64_t chi) {
+                                                 uint64_t chi, uint32_t* pick) {
     const uint64_t W = a.W;
     const uint64_t need = clo + a.first_len_at + 8;
+    *pick = ~0u;
     if (need > W) return 0;
     const uint64_t lim0 = W - need;
     const uint64_t jmax = min<uint64_t>(chi - clo, W - need + 1);
@@ -476,12 +480,22 @@ __device__ __forceinline__ uint64_t chunk_mask_z(const SxArgs& a, const uint8_t*
         return (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(w2, w1, s3)) << 32) |
                __builtin_amdgcn_alignbyte(w1, w0, s3);
     };
+    uint32_t j0 = ~0u;
+    uint64_t best = ~0ull;
     while (cand) {
         const uint32_t j = __builtin_ctzll(cand);
         cand &= cand - 1;
-        if (u64_at(o + j) + j > lim0) continue;
+        const uint64_t len = u64_at(o + j);
+        if (len + j > lim0) continue;
         if (a.prefix_len && ((u64_at(at + j) ^ a.pre8) & pm)) continue;
         mask |= 1ull << j;
+        // the first cluster's pick (k_sx_spec): of the passing positions
+        // within 8 bytes of the first, the smallest first string length
+        if (j0 == ~0u) j0 = j;
+        if (j < j0 + 8 && len < best) {
+            best = len;
+            *pick = j;
+        }
     }
     return mask;
 }
@@ -522,9 +536,16 @@ __device__ __forceinline__ uint32_t next_bit(const uint64_t* m, uint32_t i) {
 // after its records, stop bits, the exclusive scans of records and chars, and
 // 256-bit masks: chunks with a start, segment tails, chunks a chain jumped.
 template <int NC>
-struct Chunks {
+struct ChunkChars {
+    uint64_t pch[NC][kBlock + 1];
+};
+template <>
+struct ChunkChars<0> {  // no chars scans (never indexed: loops over k < NC)
+    uint64_t pch[1][1];
+};
+template <int NC>
+struct Chunks : ChunkChars<NC> {
     uint64_t exit[kBlock];
-    uint64_t pch[NC ? NC : 1][kBlock + 1];
     uint32_t pcnt[kBlock + 1];
     uint16_t start[kBlock];
     uint8_t stop[kBlock];
@@ -749,11 +770,13 @@ __device__ __forceinline__ void link_chunks(Chunks<NC>& L, uint64_t b0, uint64_t
     const uint64_t x = block_xscan(ccnt, &tot, L.ws);
     L.pcnt[tid] = static_cast<uint32_t>(x);
     if (tid == 0) L.pcnt[kBlock] = static_cast<uint32_t>(tot);
+    if constexpr (NC > 0) {
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-        const uint64_t y = block_xscan(cch[k], &tot, L.ws);
-        L.pch[k][tid] = y;
-        if (tid == 0) L.pch[k][kBlock] = tot;
+        for (int k = 0; k < NC; ++k) {
+            const uint64_t y = block_xscan(cch[k], &tot, L.ws);
+            L.pch[k][tid] = y;
+            if (tid == 0) L.pch[k][kBlock] = tot;
+        }
     }
     __syncthreads();
 }
@@ -764,6 +787,7 @@ struct SpecLds {
     alignas(16) uint8_t st[kStage + 16];  // wire bytes [base, base + kStage)
     alignas(16) uint8_t pre[kMaxPrefix + 16];
     Chunks<NC> c;
+    uint8_t list[kBlock * kListCap];       // per chunk: its records' starts (offsets in the chunk)
 };
 
 template <int NC>
@@ -789,24 +813,28 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
             sp = 0;  // the stream starts at 0: no speculation
         } else {
             const uint32_t at = static_cast<uint32_t>(clo - rd.base);
-            uint64_t mask = W < (1ull << 32) && !(a.mode & 4) ? chunk_mask_z(a, L.st, at, clo, chi)
-                                                               : chunk_mask(a, L.st, at, clo, chi);
+            uint32_t pj = ~0u;
+            const bool zf = W < (1ull << 32) && !(a.mode & 4);
+            uint64_t mask = zf ? chunk_mask_z(a, L.st, at, clo, chi, &pj) : chunk_mask(a, L.st, at, clo, chi);
             const uint64_t passing = mask;
             // the first cluster of passing positions (8 bytes from the first):
             // its smallest first string length is the true start (a start
             // 1-3 bytes early reads the true length shifted up), tested first
             // -- one plausibility test per chunk on random data
             if (mask) {
-                const uint32_t j0 = __builtin_ctzll(mask);
-                uint64_t cl = (mask >> j0) & 0xff;
-                uint64_t best = ~0ull, pick = ~0ull;
-                while (cl) {
-                    const uint64_t q = clo + j0 + __builtin_ctzll(cl);
-                    cl &= cl - 1;
-                    const uint64_t l = so.u64(q + a.first_len_at);
-                    if (l < best) {
-                        best = l;
-                        pick = q;
+                uint64_t pick = pj != ~0u ? clo + pj : ~0ull;
+                if (!zf) {
+                    const uint32_t j0 = __builtin_ctzll(mask);
+                    uint64_t cl = (mask >> j0) & 0xff;
+                    uint64_t best = ~0ull;
+                    while (cl) {
+                        const uint64_t q = clo + j0 + __builtin_ctzll(cl);
+                        cl &= cl - 1;
+                        const uint64_t l = so.u64(q + a.first_len_at);
+                        if (l < best) {
+                            best = l;
+                            pick = q;
+                        }
                     }
                 }
                 uint32_t err = SRPC_STATUS_BOUNDS;
@@ -861,7 +889,8 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     if (sq1 != ~0ull) {  // the first record was parsed by the test above: walk on from its end
 #pragma unroll
         for (int k = 0; k < NC; ++k) cch[k] = sch1[k];
-        walk_chunk<NC>(a, rd, sq1, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+        L.list[tid * kListCap] = static_cast<uint8_t>(sp - clo);
+        walk_chunk<NC>(a, rd, sq1, chi, &ccnt, &cexit, cch, &cstop, L.list + tid * kListCap + 1);
         if (sq1 >= chi) {  // (the walk saw no record: cexit = ~0)
             ccnt = 0;
             cexit = sq1;
@@ -869,7 +898,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
         }
         ++ccnt;
     } else {
-        walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+        walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, L.list + tid * kListCap);
     }
     Chunks<NC>& C = L.c;
     C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
@@ -880,6 +909,14 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     __syncthreads();
     SXP(1);
     link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
+    // the chunks' records in order (the block's whole record list when its
+    // chunks form one segment: k_sx_decode's fast path takes it from here)
+    {
+        const uint32_t r0 = C.pcnt[tid];
+        uint16_t* rl = S.rl + b * kMaxRec;
+        for (uint32_t k = 0; k < ccnt && r0 + k < kMaxRec; ++k)
+            rl[r0 + k] = static_cast<uint16_t>(tid * kSC + L.list[tid * kListCap + k]);
+    }
     SXP(2);
 
     // the table (wave 0, lane = window position): every plausible position of
@@ -941,7 +978,8 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
         uint64_t* h = S.hdr + 4 * b;
         h[0] = wmask;
         h[1] = sF;
-        h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull);
+        h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull) |
+               (static_cast<uint64_t>(min<uint32_t>(C.pcnt[kBlock], kMaxRec)) << 32);
     }
     SXP(3);
 }
@@ -1351,23 +1389,27 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
 // ---- phase 3: the records of every block ----------------------------------------
 template <int NC>
 struct DecLds {
-    alignas(16) uint8_t st[kStage + 16];
     alignas(16) uint8_t pre[kMaxPrefix + 16];
-    alignas(16) uint8_t img[kImage + 32];  // chars image; the explicit start list while walking
+    alignas(16) uint8_t st[kStage + 16];
     union {
         struct {  // until the block's records are listed in tbl
             Chunks<0> c;
             uint8_t list[kBlock * kListCap];
+            uint16_t xl[kMaxRec];  // the chain's explicit starts
         } w;
-        uint32_t loff[kMaxRec + 1];  // then: per local record, a chars offset (field being copied)
+        struct {  // then, per local record of the string field being copied:
+            uint32_t loff[kMaxRec + 1];  // its chars' offset in the block's run of chars
+            uint16_t src[kMaxRec];       // where its chars are on the wire, from the block start
+                                         // (kFar: 64 KiB or more, found again from the record)
+        } s;
     } u;
-    uint16_t tbl[kMaxRec + 1];  // the block's records in order: offset from the block
+    alignas(8) uint16_t tbl[kMaxRec + 4];  // the block's records in order: offset from the block
     uint64_t ws[kBlock / 64];
     uint32_t s_nexp;
 };
 
 template <int NC, bool kDecode>
-__global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+__global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
                                                       srpc_unpack_status* st) {
     __shared__ DecLds<NC> L;
     constexpr uint32_t E = ew<NC>();
@@ -1403,25 +1445,24 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     const uint64_t x = s.x, R = s.cnt;
     if ((s.stop & 1) || x >= b1 || R > n) return;  // no record of the batch starts here
     Chunks<0>& C = L.u.w.c;
+    uint32_t nrec;
+    if (((hmeta >> 16) & 1) && x == hsF) {
+        // entered at the first speculated start of a block whose chunks form
+        // one segment: every chunk's records, in order, are the block's --
+        // phase 1 listed them
+        nrec = static_cast<uint32_t>((hmeta >> 32) & 0xFFFF);
+        const uint64_t* rl = reinterpret_cast<const uint64_t*>(S.rl + b * kMaxRec);
+        for (uint32_t k = tid; 4 * k < nrec; k += kBlock) reinterpret_cast<uint64_t*>(L.tbl)[k] = rl[k];
+        __syncthreads();
+        SXP(9);
+        SXP(10);
+    } else {
     // every chunk again from its speculated start (phase 1's byte)
     const uint64_t sp = sb == kNoSpec ? ~0ull : clo + sb;
     uint64_t cch[kMaxNC + 1] = {};
     uint32_t ccnt, cstop;
     uint64_t cexit;
     walk_chunk<0>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, L.u.w.list + tid * kListCap);
-    uint32_t nrec;
-    if (((hmeta >> 16) & 1) && x == hsF) {
-        // entered at the first speculated start of a block whose chunks form
-        // one segment: every chunk's records, in order, are the block's
-        uint64_t tot;
-        const uint32_t fb = static_cast<uint32_t>(block_xscan(ccnt, &tot, L.ws));
-        for (uint32_t k = 0; k < ccnt; ++k)
-            L.tbl[fb + k] = static_cast<uint16_t>(tid * kSC + L.u.w.list[tid * kListCap + k]);
-        __syncthreads();
-        nrec = static_cast<uint32_t>(min<uint64_t>(tot, kMaxRec));
-        SXP(9);
-        SXP(10);
-    } else {
     C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
     C.exit[tid] = cexit;
     C.stop[tid] = static_cast<uint8_t>(cstop);
@@ -1433,9 +1474,9 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     link_chunks<0>(C, b0, sp, cexit, cstop, ccnt, cch);
     SXP(10);
 
-    // the chain from the block's entry: explicit starts (in the image area
-    // until the table is built) and the chunks it jumped
-    uint16_t* xl = reinterpret_cast<uint16_t*>(L.img);
+    // the chain from the block's entry: explicit starts (xl, until the table is
+    // built) and the chunks it jumped
+    uint16_t* xl = L.u.w.xl;
     if (tid == 0) {
         uint32_t ne = 0;
         (void)walk_chain<0, true>(a, rd, C, b0, b1, x, xl, &ne);
@@ -1476,10 +1517,14 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     }
     SXP(11);
 
-    // records r = R + k of the batch, up to index n (record n's start)
+    // records r = R + k of the batch, up to index n (record n's start); the
+    // first string field's lengths and chars positions on the way (the
+    // strings pass below takes them from here)
+    uint32_t huge0 = 0;
     for (uint32_t k = tid; k < nrec; k += kBlock) {
         const uint64_t r = R + k;
-        if (r > n) break;
+        if (kDecode && r >= n) L.u.s.loff[k] = 0;  // (no chars: not a record of the batch)
+        if (r > n) continue;
         const uint64_t sr = b0 + L.tbl[k];
         a.rec_offs[r] = sr;
         if (!kDecode || r == n) continue;
@@ -1497,6 +1542,11 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
                 }
                 pos += sz;
             } else {
+                if (a.sord[f] == 0) {
+                    huge0 |= (v >> kHugeLog2) | ((pos + 8 - b0) >> 31) ? 1u : 0u;
+                    L.u.s.loff[k] = static_cast<uint32_t>(v);
+                    L.u.s.src[k] = static_cast<uint16_t>(min<uint64_t>(pos + 8 - b0, kFar));
+                }
                 pos += 8 + v;
             }
         }
@@ -1504,7 +1554,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
     SXP(12);
     if constexpr (kDecode) {
         // per string field: local offsets (a scan over the block's records),
-        // str_offs, the chars image, aligned stores
+        // str_offs, each record's chars copied from the stage by its lane
         uint64_t Pbase[kMaxNC + 1];
         {
             uint64_t sum = 0;
@@ -1524,8 +1574,10 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
             uint64_t P = 0;
 #pragma unroll
             for (int k = 0; k <= NC; ++k) P = si == static_cast<uint32_t>(k) ? Pbase[k] : P;
-            // lengths of this field (strided: lane per record)
-            for (uint32_t k = tid; k < nrec; k += kBlock) {
+            // this field's length and where its chars are, lane per record
+            // (string ordinal 0: from the fixed-field pass)
+            uint32_t huge = si == 0 ? huge0 : 0;
+            for (uint32_t k = tid; k < nrec && si != 0; k += kBlock) {
                 uint64_t pos = b0 + L.tbl[k] + a.prefix_len, len = 0;
                 for (uint32_t g = 0; g <= f; ++g) {
                     const uint32_t sz = a.size[g];
@@ -1536,94 +1588,101 @@ __global__ __launch_bounds__(kBlock) void k_sx_decode(SxArgs a, const uint8_t* _
                     len = rd.u64(pos);
                     pos += 8 + (g < f ? len : 0);
                 }
-                L.u.loff[k] = k < nw ? static_cast<uint32_t>(len) : 0;
+                len = k < nw ? len : 0;
+                huge |= (len >> kHugeLog2) | ((pos - b0) >> 31) ? 1u : 0u;
+                L.u.s.loff[k] = static_cast<uint32_t>(len);
+                L.u.s.src[k] = static_cast<uint16_t>(min<uint64_t>(pos - b0, kFar));
             }
-            __syncthreads();
+            uint64_t* so = a.soff[f];
+            uint8_t* chars = a.col[f];
+            if (__syncthreads_or(huge)) {
+                // a string of 8 KiB or more: the records one at a time (64-bit
+                // offsets, the whole block copying each one's chars)
+                uint64_t off = 0;
+                for (uint32_t k = 0; k < nrec; ++k) {
+                    uint64_t pos = b0 + L.tbl[k] + a.prefix_len, len = 0;
+                    for (uint32_t g = 0; g <= f; ++g) {
+                        const uint32_t sz = a.size[g];
+                        if (sz) {
+                            pos += sz;
+                            continue;
+                        }
+                        len = rd.u64(pos);
+                        pos += 8 + (g < f ? len : 0);
+                    }
+                    len = k < nw ? len : 0;
+                    if (tid == 0 && R + k <= n) so[R + k] = P + off;
+                    for (uint64_t i = tid; i < len; i += kBlock) chars[P + off + i] = rd.u8(pos + i);
+                    off += len;
+                }
+                __syncthreads();
+                continue;
+            }
             // contiguous per lane: serial sums, then the block scan
             uint64_t mysum = 0;
             const uint32_t k0 = min(tid * per, nrec), k1 = min(k0 + per, nrec);
-            for (uint32_t k = k0; k < k1; ++k) mysum += L.u.loff[k];
+            for (uint32_t k = k0; k < k1; ++k) mysum += L.u.s.loff[k];
             uint64_t ftot;
             uint64_t run = block_xscan(mysum, &ftot, L.ws);
             for (uint32_t k = k0; k < k1; ++k) {
-                const uint32_t len = L.u.loff[k];
-                L.u.loff[k] = static_cast<uint32_t>(run);
+                const uint32_t len = L.u.s.loff[k];
+                L.u.s.loff[k] = static_cast<uint32_t>(run);
                 run += len;
             }
-            if (tid == 0) L.u.loff[nrec] = static_cast<uint32_t>(ftot);
+            if (tid == 0) L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
             __syncthreads();
-            uint64_t* so = a.soff[f];
-            uint8_t* chars = a.col[f];
-            for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.loff[k];
-            const bool fits = ftot + 32 <= kImage;
-            // each record's chars into the image (or straight to the output)
+            for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.s.loff[k];
+            // lane per record: its chars straight from the stage to the column
+            // (byte, dword and aligned 16-byte stores)
             for (uint32_t k = tid; k < nw; k += kBlock) {
-                const uint32_t o = L.u.loff[k], len = L.u.loff[k + 1] - o;
+                const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
                 if (!len) continue;
-                const uint64_t sr = b0 + L.tbl[k];
-                uint64_t pos = sr + a.prefix_len;
-                for (uint32_t g = 0; g < f; ++g) pos += a.size[g] ? a.size[g] : 8 + rd.u64(pos);
-                pos += 8;
-                if (fits) {
-                    const uint32_t d = 16 + o;
-                    if (rd.staged(pos, pos + len)) {
-                        uint8_t* l0 = reinterpret_cast<uint8_t*>(&L);
-                        lds_copy_run(l0, static_cast<uint32_t>(L.img - l0) + d,
-                                     static_cast<uint32_t>(L.st - l0) + static_cast<uint32_t>(pos - rd.base), len);
-                    } else {
-                        for (uint32_t x8 = 0; x8 < len; x8 += 8) {
-                            const uint32_t kk = min<uint32_t>(8, len - x8);
-                            uint64_t v = 0;
-                            for (uint32_t bb = 0; bb < kk; ++bb) v |= static_cast<uint64_t>(w[pos + x8 + bb]) << (8 * bb);
-                            lds_put_small(L.img, d + x8, v, kk);
-                        }
-                    }
-                } else {
-                    uint8_t* dst = chars + P + o;
-                    for (uint32_t bb = 0; bb < len; ++bb) dst[bb] = rd.u8(pos + bb);
+                uint8_t* d = chars + P + o;
+                uint64_t sp = b0 + L.u.s.src[k];
+                if (L.u.s.src[k] == kFar) {
+                    sp = b0 + L.tbl[k] + a.prefix_len;
+                    for (uint32_t g = 0; g < f; ++g) sp += a.size[g] ? a.size[g] : 8 + rd.u64(sp);
+                    sp += 8;
                 }
-            }
-            __syncthreads();
-            if (fits && ftot) {
-                // chunk c of the output covers image bytes [16c - h, 16c + 16 - h)
-                const uint32_t h = static_cast<uint32_t>(P & 15);
-                const uint64_t gbase = P & ~15ull;
-                const uint8_t* im = L.img + 16;
-                const uint32_t span = h + static_cast<uint32_t>(ftot);
-                const uint32_t nch = (span + 15) >> 4;
-                const uint32_t sh = (16 - h) & 15;
-                for (uint32_t c = tid; c < nch; c += kBlock) {
-                    const uint32_t lo = max(h, 16 * c), hi2 = min(span, 16 * c + 16);
-                    if (lo == 16 * c && hi2 == 16 * c + 16) {
-                        const uint32_t* wd = reinterpret_cast<const uint32_t*>(im + 16 * c - h - sh);
-                        const uint32_t w0 = wd[0], w1 = wd[1], w2 = wd[2], w3 = wd[3], w4 = wd[4], w5 = wd[5],
-                                       w6 = wd[6], w7 = wd[7];
-                        uint32_t o0, o1, o2, o3;
-                        const uint32_t bsh = sh & 3;
-                        switch (sh >> 2) {  // uniform
-                        case 0:
-                            o0 = __builtin_amdgcn_alignbyte(w1, w0, bsh); o1 = __builtin_amdgcn_alignbyte(w2, w1, bsh);
-                            o2 = __builtin_amdgcn_alignbyte(w3, w2, bsh); o3 = __builtin_amdgcn_alignbyte(w4, w3, bsh);
-                            break;
-                        case 1:
-                            o0 = __builtin_amdgcn_alignbyte(w2, w1, bsh); o1 = __builtin_amdgcn_alignbyte(w3, w2, bsh);
-                            o2 = __builtin_amdgcn_alignbyte(w4, w3, bsh); o3 = __builtin_amdgcn_alignbyte(w5, w4, bsh);
-                            break;
-                        case 2:
-                            o0 = __builtin_amdgcn_alignbyte(w3, w2, bsh); o1 = __builtin_amdgcn_alignbyte(w4, w3, bsh);
-                            o2 = __builtin_amdgcn_alignbyte(w5, w4, bsh); o3 = __builtin_amdgcn_alignbyte(w6, w5, bsh);
-                            break;
-                        default:
-                            o0 = __builtin_amdgcn_alignbyte(w4, w3, bsh); o1 = __builtin_amdgcn_alignbyte(w5, w4, bsh);
-                            o2 = __builtin_amdgcn_alignbyte(w6, w5, bsh); o3 = __builtin_amdgcn_alignbyte(w7, w6, bsh);
-                            break;
-                        }
-                        __builtin_nontemporal_store(u32x4{o0, o1, o2, o3},
-                                                    reinterpret_cast<u32x4*>(chars + gbase + 16 * c));
-                    } else {
-                        for (uint32_t xx = lo; xx < hi2; ++xx) chars[gbase + xx] = im[xx - h];
-                    }
+                if (!rd.staged(sp, sp + len)) {
+                    for (uint32_t i = 0; i < len; ++i) d[i] = rd.u8(sp + i);
+                    continue;
                 }
+                const uint32_t so = static_cast<uint32_t>(sp - rd.base);
+                const uint32_t head = min<uint32_t>(len, (4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+                uint32_t i = 0;
+#pragma nounroll
+                for (; i < head; ++i) d[i] = rd.lds[so + i];
+                // from here d + i is 4-aligned: dwords, 16-byte pieces once it is
+                // 16-aligned, dwords, bytes
+                const uint32_t sa = (so + i) & 3;
+                lds_u32c* sw = reinterpret_cast<lds_u32c*>(rd.lds + ((so + i) & ~3u));
+                uint32_t* dw = reinterpret_cast<uint32_t*>(d + i);
+                uint32_t nd = (len - i) >> 2;
+                uint32_t w0 = sw[0], j = 0;
+                const uint32_t pre = min<uint32_t>(nd, ((16 - (reinterpret_cast<uintptr_t>(dw) & 15)) & 15) >> 2);
+#pragma nounroll
+                for (; j < pre; ++j) {
+                    const uint32_t w1 = sw[j + 1];
+                    dw[j] = __builtin_amdgcn_alignbyte(w1, w0, sa);
+                    w0 = w1;
+                }
+#pragma nounroll
+                for (; j + 4 <= nd; j += 4) {
+                    const uint32_t w1 = sw[j + 1], w2 = sw[j + 2], w3 = sw[j + 3], w4 = sw[j + 4];
+                    *reinterpret_cast<u32x4*>(dw + j) =
+                        u32x4{__builtin_amdgcn_alignbyte(w1, w0, sa), __builtin_amdgcn_alignbyte(w2, w1, sa),
+                              __builtin_amdgcn_alignbyte(w3, w2, sa), __builtin_amdgcn_alignbyte(w4, w3, sa)};
+                    w0 = w4;
+                }
+#pragma nounroll
+                for (; j < nd; ++j) {
+                    const uint32_t w1 = sw[j + 1];
+                    dw[j] = __builtin_amdgcn_alignbyte(w1, w0, sa);
+                    w0 = w1;
+                }
+#pragma nounroll
+                for (i += 4 * nd; i < len; ++i) d[i] = rd.lds[so + i];
             }
             __syncthreads();
         }
@@ -1638,7 +1697,7 @@ __global__ void k_zero_ctl(uint64_t* ctl) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct SxLayout {
-    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, total;
+    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, total;
 };
 
 SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
@@ -1663,6 +1722,8 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     o += r256(8 * E * L.nb);
     L.ctl = o;
     o += r256(8 * kCtlWords);
+    L.rl = o;
+    o += r256(2 * kMaxRec * L.nb);
     L.total = o;
     return L;
 }
@@ -1686,36 +1747,21 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
 }  // namespace
 }  // namespace srpc_impl
 
-// The old decoders (stream.hip: chunk pipeline + indexed decode, sdec.hip,
-// stream1.hip), kept callable for A/B measurements through
-// srpc_debug_stream_force_single(1..6) until they are removed.
-extern "C" int srpc_legacy_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out);
-extern "C" int srpc_legacy_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
-                                             uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
-                                             srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes,
-                                             void* stream);
-extern "C" int srpc_legacy_stream_mode();
-
 using namespace srpc_impl;
 
 extern "C" {
 
 int srpc_plan_var_stream_scratch_bytes(const srpc_plan* p, uint64_t n, uint64_t wire_len, uint64_t* out) {
     if (!p || !out || !p->has_string) return SRPC_E_INVALID;
-    uint64_t var = 0, legacy = 0;
+    uint64_t var = 0;
     if (int rc = srpc_plan_var_scratch_bytes(p, n, wire_len, &var)) return rc;
-    if (int rc = srpc_legacy_var_stream_scratch_bytes(p, n, wire_len, &legacy)) return rc;
-    const uint64_t mine = (sx_decodes(p) ? 0 : r256(var)) + sx_layout(wire_len, sx_decodes(p) ? p->nstrings - 1 : 0).total;
-    *out = std::max(mine, legacy);
+    *out = (sx_decodes(p) ? 0 : r256(var)) + sx_layout(wire_len, sx_decodes(p) ? p->nstrings - 1 : 0).total;
     return SRPC_OK;
 }
 
 int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, uint64_t n,
                                uint64_t* rec_offs, void* const* cols, uint64_t* const* str_offs,
                                srpc_unpack_status* st, void* scratch, uint64_t scratch_bytes, void* stream) {
-    if (srpc_legacy_stream_mode())
-        return srpc_legacy_unpack_var_stream(p, wire, wire_len, n, rec_offs, cols, str_offs, st, scratch,
-                                             scratch_bytes, stream);
     const TimedCall timed;
     if (!p || !p->has_string || !rec_offs || !scratch || !cols || !str_offs) return SRPC_E_INVALID;
     if (wire_len && !wire) return SRPC_E_INVALID;
@@ -1743,7 +1789,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
                 reinterpret_cast<uint64_t*>(base + SL.gp),
                 reinterpret_cast<uint64_t*>(base + SL.gin),
                 reinterpret_cast<uint64_t*>(base + SL.bst),
-                reinterpret_cast<uint64_t*>(base + SL.ctl)};
+                reinterpret_cast<uint64_t*>(base + SL.ctl),
+                reinterpret_cast<uint16_t*>(base + SL.rl)};
     SxArgs a{};
     uint32_t si = 0;
     for (uint32_t f = 0; f < p->nfields; ++f) {
@@ -1764,7 +1811,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
     for (uint32_t f = 0; f < p->nfields && p->size[f]; ++f) a.first_len_at += p->size[f];
     a.plaus = p->prefix_len >= 8 ? kPlausPrefixed : kPlausBare;
     for (uint32_t i = 0; i < 8 && i < p->prefix_len; ++i) a.pre8 |= static_cast<uint64_t>(p->h_prefix[i]) << (8 * i);
-    a.cap = 1 + kSC / p->fixed_bytes;
+    a.cap = (kSC + p->fixed_bytes - 1) / p->fixed_bytes;  // <= kListCap (fixed_bytes >= 8)
     {
         uint32_t k = 0, run = p->prefix_len;
         for (uint32_t f = 0; f < p->nfields; ++f) {

@@ -60,7 +60,8 @@ def layout(recs, nfields):
     # Number's fields cover the struct (no read-back of the struct tile)
     ("quad", None, False, 0), ("number", "response", False, 0), ("all", "request", False, 0),
     # all six kinds, plain and behind a vtable slot, no envelope: the
-    # compile-time layout kernels (rec.hip) for whole tiles, staged ones for the rest
+    # compile-time layout kernels (aos.hip k_*_aos_lay; n = 1..100003 covers
+    # the array's last, partial lane)
     ("all", None, False, 0),
     # a struct array 8 bytes off 16-byte alignment: the per-field kernels
     ("quad", None, True, 8), ("all", "request", True, 8)])
@@ -112,7 +113,8 @@ def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
 @pytest.mark.parametrize("n", [1, 17, 4099, 100_003])
 @pytest.mark.parametrize("schema,envelope,vptr,shift", [
     ("quad", None, True, 0),          # the run kernel (fields one run behind the vtable slot)
-    ("all", None, True, 0), ("all", "request", True, 0), ("i64_i8", None, True, 0),  # staged kernels
+    ("all", None, True, 0), ("all", None, False, 0),  # layout kernels (k_unpack_aos_lay<L, true>)
+    ("all", "request", True, 0), ("i64_i8", None, True, 0),  # staged kernels
     ("quad", None, False, 0),         # fields cover the struct: no fill needed
     ("quad", None, True, 8), ("all", "request", True, 8)])  # per-field kernels (+ a fill pass)
 def test_aos_unpack_into_fresh_objects(n, schema, envelope, vptr, shift):

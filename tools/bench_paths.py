@@ -209,6 +209,25 @@ def main():
                    "pack_GBps": round(alg / tp / 1e9, 1), "unpack_GBps": round(alg / tu / 1e9, 1),
                    "pack_frac": round(alg / tp / 8e12, 4), "unpack_frac": round(alg / tu / 8e12, 4),
                    "parity_ok": bool(ok)}
+            if sum(k == oracle.STRING for k in kinds) > 1:
+                # several string fields: the unpack with the batch's tile table
+                # (srpc_gpu_unpack_var_tiled, ABI 6; the table from the pack's
+                # own input offsets), checked against the look-back unpack
+                tw = p.var_tile_table_words(n)
+                table = torch.empty(8 * tw + 16, dtype=torch.uint8, device=dev)
+                p.var_tile_table(doffs, n, table, stream=s)
+                p.unpack_var(wire, total, n, rec, outs, ooffs, scratch, sb, stream=s)
+                torch.cuda.synchronize()
+                ref = [o.clone() for o in outs], [o.clone() if o is not None else None for o in ooffs]
+                for o in outs:
+                    o.fill_(0)
+                tt = timeit(lambda: p.unpack_var_tiled(wire, total, n, rec, table, outs, ooffs, scratch, sb,
+                                                       stream=s))
+                torch.cuda.synchronize()
+                same = all(torch.equal(a, b) for a, b in zip(outs, ref[0])) and all(
+                    a is None or torch.equal(a, b) for a, b in zip(ooffs, ref[1]))
+                row["parity_ok"] = row["parity_ok"] and same
+                row.update({"unpack_tiled_us": round(tt * 1e6, 2), "unpack_tiled_frac": round(alg / tt / 8e12, 4)})
             if args.stream:
                 # the same wire decoded with NO record index (srpc_gpu_unpack_var_stream),
                 # the index rebuilt on the device and written out (8 B per record more)
@@ -254,6 +273,8 @@ def main():
             f.write(txt)
     for r in rows:
         extra = f'  stream {r["stream_us"]:8.1f} us ({r["stream_frac"]:.3f})' if "stream_us" in r else ""
+        if "unpack_tiled_us" in r:
+            extra += f'  unpack_tiled {r["unpack_tiled_us"]:8.1f} us ({r["unpack_tiled_frac"]:.3f})'
         if "unpack_fill_us" in r:
             extra += f'  unpack_fill {r["unpack_fill_us"]:8.1f} us ({r["unpack_fill_frac"]:.3f})'
         if "generic_pack_frac" in r:

@@ -68,10 +68,6 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--single", type=int, default=0,
-                    help="decoders (srpc_debug_stream_force_single, stream.hip): 0 default, 2 the bounded "
-                         "pass alone, 3 chunk pipeline -> bounded pass, 4 the speculative pass never giving "
-                         "up, 5 speculative pass -> bounded pass, 6 default with the hand-over forced")
     ap.add_argument("--tables", type=int, default=0,
                     help="srpc_debug_stream_tables bits (sdx.hip): 1 sF-only tables, 2 empty tables, "
                          "4 the exact speculation filter")
@@ -84,11 +80,6 @@ def main():
     import srpc_amd
     from srpc_amd import GpuPacker, Schema
 
-    if args.single:
-        import ctypes
-        hook = srpc_amd._lib.lib().srpc_debug_stream_force_single
-        hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
-        hook(args.single)
     if args.tables:
         import ctypes
         th = srpc_amd._lib.lib().srpc_debug_stream_tables
@@ -162,11 +153,12 @@ def main():
         alg = W + col_bytes + str_bytes + 8 * (n + 1) * nstr + 8 * (n + 1)
         row = {"case": name, "records": n, "wire_bytes": W, "alg_bytes": alg, "us": round(t * 1e6, 2),
                "GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 8e12, 4), "parity_ok": bool(ok),
-               "blocks": (W + 8191) // 8192, "missed_blocks": reserved >> 8, "diag_bits": reserved & 7,
-               "single_pass": bool(reserved & 2), "gave_up": bool(reserved & 8)}
+               "blocks": (W + 8191) // 8192, "walk_waves": reserved >> 8, "diag_bits": reserved & 3,
+               "off_primary": bool(reserved & 1), "walked_miss": bool(reserved & 2)}
         rows.append(row)
         print(f'{name:36s} {n:9d} rec {W / 2**20:8.1f} MiB  {row["us"]:9.1f} us  {row["GBps"]:7.1f} GB/s '
-              f'({row["frac"]:.3f})  parity={ok}  bounded={row["single_pass"]} gave_up={row["gave_up"]} missed {row["missed_blocks"]}/{row["blocks"]}',
+              f'({row["frac"]:.3f})  parity={ok}  off_primary={row["off_primary"]} walked={row["walked_miss"]} '
+              f'walk_waves {row["walk_waves"]}/{row["blocks"]} blocks',
               flush=True)
 
     S, I8, C8, I16, I32, I64 = oracle.STRING, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64
