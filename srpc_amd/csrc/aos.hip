@@ -271,7 +271,10 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
 // on the all-kinds struct: profiles/r04_pmc_aos.txt).  For the struct layouts
 // the benchmarks and the reference's examples use, the layout is a template
 // instead (as rec.hip does for columns): a lane holds G structs in registers
-// (16-byte loads straight from HBM; the wave's loads cover whole lines), builds
+// (16-byte PLAIN loads straight from HBM: the wave's loads cover whole lines,
+// which stay in the caches between its instructions -- non-temporal loads
+// refetched them, 0.35 of peak; staging the struct side through LDS instead
+// measured 0.70 pack / 0.41 fresh-object unpack: profiles/r04_aos_lay_ab.log), builds
 // its G wire records as dwords with byte permutes fixed at compile time, and
 // the wave streams its wire tile through LDS in coalesced 16-byte pieces (an
 // odd dword stride per lane: no bank conflicts).  Unpack is the mirror; bytes
@@ -608,16 +611,10 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos_staged(AosArgs a, const u
 
 // Staged-kernel tiling: R (a multiple of 16) records whose two images fill
 // about kAosTileBytes of LDS; returns the LDS bytes, sets a->R / a->simg.
-constexpr uint32_t kAosTileBytes = 24 * 1024;
-// A/B knob (SRPC_AOS_TILE_BYTES at load): the two images' budget
-const uint32_t g_aos_tile_bytes = [] {
-    const char* e = std::getenv("SRPC_AOS_TILE_BYTES");
-    const long v = e ? std::atol(e) : 0;
-    return v >= 1024 && v <= 64 * 1024 ? static_cast<uint32_t>(v) : kAosTileBytes;
-}();
+constexpr uint32_t kAosTileBytes = 24 * 1024;  // (12 / 16 KiB measured slower: profiles/r04_aos_lay_ab.log)
 uint32_t staged_tiling(AosArgs* a) {
     const uint32_t per = a->ident ? a->wstride : a->wstride + a->rstride;
-    uint32_t R = std::max<uint32_t>(16, (g_aos_tile_bytes / per) & ~15u);
+    uint32_t R = std::max<uint32_t>(16, (kAosTileBytes / per) & ~15u);
     a->R = R;
     const uint32_t wimg = (R * a->wstride + 15) & ~15u;
     a->simg = a->ident ? 0 : wimg;

@@ -69,6 +69,7 @@ constexpr int kMaxNC = 3;                        // chars values carried per sta
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
 constexpr uint32_t kHugeLog2 = 13;               // strings from 8 KiB: copied by the whole block
 constexpr uint16_t kFar = 0xFFFF;
+constexpr uint32_t kWaveCopyAvg = 128;  // chars per record from which the decode copies a wave per record
 constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint16_t kNoStart = 0xFFFF;
 constexpr uint8_t kNoSpec = 0xFF;
@@ -1632,6 +1633,39 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
             if (tid == 0) L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
             __syncthreads();
             for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.s.loff[k];
+            if (ftot >= static_cast<uint64_t>(kWaveCopyAvg) * nw) {
+                // long strings (few records): a wave per record, a lane per
+                // 16-byte aligned piece of the column, read unaligned from the
+                // stage (the record's first / last piece byte by byte: the
+                // neighbouring records own the other bytes)
+                const uint32_t lane = tid & 63;
+                for (uint32_t k = tid >> 6; k < nw; k += kBlock / 64) {
+                    const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
+                    if (!len) continue;
+                    uint64_t sp = b0 + L.u.s.src[k];
+                    if (L.u.s.src[k] == kFar) {
+                        sp = b0 + L.tbl[k] + a.prefix_len;
+                        for (uint32_t g = 0; g < f; ++g) sp += a.size[g] ? a.size[g] : 8 + rd.u64(sp);
+                        sp += 8;
+                    }
+                    const uint64_t d0 = P + o, d1 = d0 + len;  // column bytes [d0, d1)
+                    const bool staged = rd.staged(sp, sp + len);
+                    for (uint64_t c = (d0 & ~15ull) + 16 * lane; c < d1; c += 16 * 64) {
+                        if (c >= d0 && c + 16 <= d1 && staged) {
+                            const uint32_t so = static_cast<uint32_t>(sp + (c - d0) - rd.base);
+                            lds_u32c* q = reinterpret_cast<lds_u32c*>(rd.lds + (so & ~3u));
+                            const uint32_t s3 = so & 3, w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+                            // plain stores: the L2 merges them with the neighbours' edge bytes
+                            *reinterpret_cast<u32x4*>(chars + c) =
+                                u32x4{__builtin_amdgcn_alignbyte(w1, w0, s3), __builtin_amdgcn_alignbyte(w2, w1, s3),
+                                      __builtin_amdgcn_alignbyte(w3, w2, s3), __builtin_amdgcn_alignbyte(w4, w3, s3)};
+                        } else {
+                            const uint64_t e = min<uint64_t>(c + 16, d1);
+                            for (uint64_t x = max<uint64_t>(c, d0); x < e; ++x) chars[x] = rd.u8(sp + (x - d0));
+                        }
+                    }
+                }
+            } else
             // lane per record: its chars straight from the stage to the column
             // (byte, dword and aligned 16-byte stores)
             for (uint32_t k = tid; k < nw; k += kBlock) {

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include "plan.h"
@@ -1656,8 +1657,49 @@ struct RtuArgs {
     uint32_t stage_at;   // the wire span's granules (stage_cap bytes)
     uint32_t len_at;     // per string ordinal: 256 u64 lengths, then offsets inside the tile's chars
     uint32_t img_at;     // chars image, img_cap bytes
-    uint32_t stage_cap, img_cap;
+    uint32_t stage_cap, img_cap;  // img_cap 0: no image, each record's chars copied by its lane
 };
+
+// len bytes from the LDS stage at byte offset so to global memory at d: byte
+// stores up to a 4-byte boundary of d, dwords up to a 16-byte one, 16-byte
+// stores, then dwords and bytes (the stage reads are aligned dwords funnel-
+// shifted; the stage has a dword of slack past any run).
+__device__ __forceinline__ void copy_stage_run(uint8_t* d, const uint8_t* lds, uint32_t so, uint32_t len) {
+    const lds_u8c* l8 = (const lds_u8c*)lds;
+    const uint32_t head = min<uint32_t>(len, (4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+    uint32_t i = 0;
+#pragma nounroll
+    for (; i < head; ++i) d[i] = l8[so + i];
+    typedef const uint32_t __attribute__((address_space(3))) lds_u32c;
+    const uint32_t sa = (so + i) & 3;
+    lds_u32c* sw = reinterpret_cast<lds_u32c*>(l8 + ((so + i) & ~3u));
+    uint32_t* dw = reinterpret_cast<uint32_t*>(d + i);
+    const uint32_t nd = (len - i) >> 2;
+    uint32_t w0 = sw[0], j = 0;
+    const uint32_t pre = min<uint32_t>(nd, ((16 - (reinterpret_cast<uintptr_t>(dw) & 15)) & 15) >> 2);
+#pragma nounroll
+    for (; j < pre; ++j) {
+        const uint32_t w1 = sw[j + 1];
+        dw[j] = __builtin_amdgcn_alignbyte(w1, w0, sa);
+        w0 = w1;
+    }
+#pragma nounroll
+    for (; j + 4 <= nd; j += 4) {
+        const uint32_t w1 = sw[j + 1], w2 = sw[j + 2], w3 = sw[j + 3], w4 = sw[j + 4];
+        *reinterpret_cast<u32x4*>(dw + j) =
+            u32x4{__builtin_amdgcn_alignbyte(w1, w0, sa), __builtin_amdgcn_alignbyte(w2, w1, sa),
+                  __builtin_amdgcn_alignbyte(w3, w2, sa), __builtin_amdgcn_alignbyte(w4, w3, sa)};
+        w0 = w4;
+    }
+#pragma nounroll
+    for (; j < nd; ++j) {
+        const uint32_t w1 = sw[j + 1];
+        dw[j] = __builtin_amdgcn_alignbyte(w1, w0, sa);
+        w0 = w1;
+    }
+#pragma nounroll
+    for (i += 4 * nd; i < len; ++i) d[i] = l8[so + i];
+}
 
 // General decode of record r (walk_record's multi-string semantics); string
 // ordinal si's length goes to len_l[si * 256 + lane] (its chars position is
@@ -2104,9 +2146,13 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
             const uint64_t len = (i + 1 < kBlock ? len_l[si * kBlock + i + 1] : tot) - o;
             if (len) {
                 const uint64_t pos = string_pos(a, start, si, rd);
-                const uint8_t* src = in_stage ? lds + sb + (pos - sw) : wire + pos;
                 uint8_t* dst = chars + P + o;
-                for (uint64_t k = 0; k < len; ++k) dst[k] = src[k];
+                if (in_stage) {
+                    copy_stage_run(dst, lds, sb + static_cast<uint32_t>(pos - sw), static_cast<uint32_t>(len));
+                } else {
+                    const uint8_t* src = wire + pos;
+                    for (uint64_t k = 0; k < len; ++k) dst[k] = src[k];
+                }
             }
         }
         ++si;
@@ -2281,6 +2327,13 @@ RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total, uint32_t rpl
 // tile's wire span (256 records of wire_len / n bytes with 1/16 slack); the
 // chars image one string field's chars of a tile.  Returns false when the
 // span would not fit (long records keep the walk + scans + chars kernels).
+// A/B switch (SRPC_RTU_DIRECT=1 at load): k_unpack_var_rt without the chars
+// image (more workgroups per CU; chars copied lane per record).
+const bool g_rtu_direct = [] {
+    const char* e = std::getenv("SRPC_RTU_DIRECT");
+    return e && e[0] == '1';
+}();
+
 bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total) {
     RtuArgs L{};
     const uint64_t span = std::min<uint64_t>(avg, kRtImageMax) * kBlock;
@@ -2296,10 +2349,11 @@ bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total)
     off += 8 * kBlock * p->nstrings;
     const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
     // every string field's chars of a tile, 16 bytes of slack around each
-    L.img_cap = round16(static_cast<uint32_t>(std::max<uint64_t>(1024, cap > fixed_span ? cap - fixed_span : 0) +
-                                              32 * (p->nstrings + 1)));
+    // (none when each record's lane copies its chars: SRPC_RTU_DIRECT=1)
+    L.img_cap = g_rtu_direct ? 0 : round16(static_cast<uint32_t>(
+                    std::max<uint64_t>(1024, cap > fixed_span ? cap - fixed_span : 0) + 32 * (p->nstrings + 1)));
     L.img_at = off;
-    off += L.img_cap + 32;
+    off += L.img_cap ? L.img_cap + 32 : 0;
     *out = L;
     *total = off;
     return true;
