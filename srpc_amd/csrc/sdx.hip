@@ -69,7 +69,6 @@ constexpr int kMaxNC = 3;                        // chars values carried per sta
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
 constexpr uint32_t kHugeLog2 = 13;               // strings from 8 KiB: copied by the whole block
 constexpr uint16_t kFar = 0xFFFF;
-constexpr uint32_t kWaveCopyAvg = 128;  // chars per record from which the decode copies a wave per record
 constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint16_t kNoStart = 0xFFFF;
 constexpr uint8_t kNoSpec = 0xFF;
@@ -1441,6 +1440,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
     const uint64_t hsF = S.hdr[4 * b + 1], hmeta = S.hdr[4 * b + 2];
     const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
     const uint8_t sb = clo < b1 ? S.spec[b * kBlock + tid] : kNoSpec;
+    // the record list's first 256 entries (the fast path's, read before it is
+    // known to be taken: one round trip instead of two)
+    const uint64_t* rl = reinterpret_cast<const uint64_t*>(S.rl + b * kMaxRec);
+    const uint64_t rl0 = tid < 64 ? rl[tid] : 0;
     const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);
     SXP(8);
     const uint64_t x = s.x, R = s.cnt;
@@ -1452,8 +1455,8 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
         // one segment: every chunk's records, in order, are the block's --
         // phase 1 listed them
         nrec = static_cast<uint32_t>((hmeta >> 32) & 0xFFFF);
-        const uint64_t* rl = reinterpret_cast<const uint64_t*>(S.rl + b * kMaxRec);
-        for (uint32_t k = tid; 4 * k < nrec; k += kBlock) reinterpret_cast<uint64_t*>(L.tbl)[k] = rl[k];
+        if (tid < 64 && 4 * tid < nrec) reinterpret_cast<uint64_t*>(L.tbl)[tid] = rl0;
+        for (uint32_t k = 64 + tid; 4 * k < nrec; k += kBlock) reinterpret_cast<uint64_t*>(L.tbl)[k] = rl[k];
         __syncthreads();
         SXP(9);
         SXP(10);
@@ -1633,39 +1636,6 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
             if (tid == 0) L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
             __syncthreads();
             for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.s.loff[k];
-            if (ftot >= static_cast<uint64_t>(kWaveCopyAvg) * nw) {
-                // long strings (few records): a wave per record, a lane per
-                // 16-byte aligned piece of the column, read unaligned from the
-                // stage (the record's first / last piece byte by byte: the
-                // neighbouring records own the other bytes)
-                const uint32_t lane = tid & 63;
-                for (uint32_t k = tid >> 6; k < nw; k += kBlock / 64) {
-                    const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
-                    if (!len) continue;
-                    uint64_t sp = b0 + L.u.s.src[k];
-                    if (L.u.s.src[k] == kFar) {
-                        sp = b0 + L.tbl[k] + a.prefix_len;
-                        for (uint32_t g = 0; g < f; ++g) sp += a.size[g] ? a.size[g] : 8 + rd.u64(sp);
-                        sp += 8;
-                    }
-                    const uint64_t d0 = P + o, d1 = d0 + len;  // column bytes [d0, d1)
-                    const bool staged = rd.staged(sp, sp + len);
-                    for (uint64_t c = (d0 & ~15ull) + 16 * lane; c < d1; c += 16 * 64) {
-                        if (c >= d0 && c + 16 <= d1 && staged) {
-                            const uint32_t so = static_cast<uint32_t>(sp + (c - d0) - rd.base);
-                            lds_u32c* q = reinterpret_cast<lds_u32c*>(rd.lds + (so & ~3u));
-                            const uint32_t s3 = so & 3, w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-                            // plain stores: the L2 merges them with the neighbours' edge bytes
-                            *reinterpret_cast<u32x4*>(chars + c) =
-                                u32x4{__builtin_amdgcn_alignbyte(w1, w0, s3), __builtin_amdgcn_alignbyte(w2, w1, s3),
-                                      __builtin_amdgcn_alignbyte(w3, w2, s3), __builtin_amdgcn_alignbyte(w4, w3, s3)};
-                        } else {
-                            const uint64_t e = min<uint64_t>(c + 16, d1);
-                            for (uint64_t x = max<uint64_t>(c, d0); x < e; ++x) chars[x] = rd.u8(sp + (x - d0));
-                        }
-                    }
-                }
-            } else
             // lane per record: its chars straight from the stage to the column
             // (byte, dword and aligned 16-byte stores)
             for (uint32_t k = tid; k < nw; k += kBlock) {

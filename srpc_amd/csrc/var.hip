@@ -1657,7 +1657,7 @@ struct RtuArgs {
     uint32_t stage_at;   // the wire span's granules (stage_cap bytes)
     uint32_t len_at;     // per string ordinal: 256 u64 lengths, then offsets inside the tile's chars
     uint32_t img_at;     // chars image, img_cap bytes
-    uint32_t stage_cap, img_cap;  // img_cap 0: no image, each record's chars copied by its lane
+    uint32_t stage_cap, img_cap;
 };
 
 // len bytes from the LDS stage at byte offset so to global memory at d: byte
@@ -2327,13 +2327,6 @@ RtArgs rt_layout(const srpc_plan* p, uint64_t avg, uint32_t* total, uint32_t rpl
 // tile's wire span (256 records of wire_len / n bytes with 1/16 slack); the
 // chars image one string field's chars of a tile.  Returns false when the
 // span would not fit (long records keep the walk + scans + chars kernels).
-// A/B switch (SRPC_RTU_DIRECT=1 at load): k_unpack_var_rt without the chars
-// image (more workgroups per CU; chars copied lane per record).
-const bool g_rtu_direct = [] {
-    const char* e = std::getenv("SRPC_RTU_DIRECT");
-    return e && e[0] == '1';
-}();
-
 bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total) {
     RtuArgs L{};
     const uint64_t span = std::min<uint64_t>(avg, kRtImageMax) * kBlock;
@@ -2349,11 +2342,12 @@ bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total)
     off += 8 * kBlock * p->nstrings;
     const uint64_t fixed_span = static_cast<uint64_t>(kBlock) * p->fixed_bytes;
     // every string field's chars of a tile, 16 bytes of slack around each
-    // (none when each record's lane copies its chars: SRPC_RTU_DIRECT=1)
-    L.img_cap = g_rtu_direct ? 0 : round16(static_cast<uint32_t>(
-                    std::max<uint64_t>(1024, cap > fixed_span ? cap - fixed_span : 0) + 32 * (p->nstrings + 1)));
+    // (without the image -- each record's lane copying its own chars -- the
+    // tiles ran 0.44 -> 0.32 on 0-64 B strings: fewer, wider stores won)
+    L.img_cap = round16(static_cast<uint32_t>(std::max<uint64_t>(1024, cap > fixed_span ? cap - fixed_span : 0) +
+                                              32 * (p->nstrings + 1)));
     L.img_at = off;
-    off += L.img_cap ? L.img_cap + 32 : 0;
+    off += L.img_cap + 32;
     *out = L;
     *total = off;
     return true;

@@ -8,3 +8,4 @@ timeout -k 10 60 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_default_${R}.log 2>&1 || exit 2
 bash tools/gpu_profile.sh "$R" || exit 3
 timeout -k 10 400 python3 tools/bench_paths.py --reps 10 --out gpurun_out/paths_${R}.json > gpurun_out/paths_${R}.log 2>&1 || exit 4
+timeout -k 10 300 python3 -u tools/stream_bench.py --reps 10 > gpurun_out/stream_${R}.log 2>&1 || exit 5
