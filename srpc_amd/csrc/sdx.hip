@@ -69,6 +69,7 @@ constexpr int kMaxNC = 3;                        // chars values carried per sta
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
 constexpr uint32_t kHugeLog2 = 13;               // strings from 8 KiB: copied by the whole block
 constexpr uint16_t kFar = 0xFFFF;
+constexpr uint32_t kWaveCopyAvg = 128;  // chars per record from which the decode copies a wave per record
 constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint16_t kNoStart = 0xFFFF;
 constexpr uint8_t kNoSpec = 0xFF;
@@ -104,9 +105,14 @@ __device__ unsigned long long g_sxph_blocks = 0;
             sxp_last_ = now_;                                                                      \
         }                                                                                          \
     } while (0)
+#define SXP_FLAG(i)                                                                                \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < g_sxph_blocks) g_sxph[static_cast<uint64_t>(blockIdx.x) * 16 + (i)] = 1; \
+    } while (0)
 #else
 #define SXP_BEGIN
 #define SXP(i)
+#define SXP_FLAG(i)
 #endif
 
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
@@ -1458,6 +1464,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
         if (tid < 64 && 4 * tid < nrec) reinterpret_cast<uint64_t*>(L.tbl)[tid] = rl0;
         for (uint32_t k = 64 + tid; 4 * k < nrec; k += kBlock) reinterpret_cast<uint64_t*>(L.tbl)[k] = rl[k];
         __syncthreads();
+        SXP_FLAG(15);
         SXP(9);
         SXP(10);
     } else {
@@ -1636,33 +1643,18 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
             if (tid == 0) L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
             __syncthreads();
             for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.s.loff[k];
-            // lane per record: its chars straight from the stage to the column
-            // (byte, dword and aligned 16-byte stores)
-            for (uint32_t k = tid; k < nw; k += kBlock) {
-                const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
-                if (!len) continue;
-                uint8_t* d = chars + P + o;
-                uint64_t sp = b0 + L.u.s.src[k];
-                if (L.u.s.src[k] == kFar) {
-                    sp = b0 + L.tbl[k] + a.prefix_len;
-                    for (uint32_t g = 0; g < f; ++g) sp += a.size[g] ? a.size[g] : 8 + rd.u64(sp);
-                    sp += 8;
-                }
-                if (!rd.staged(sp, sp + len)) {
-                    for (uint32_t i = 0; i < len; ++i) d[i] = rd.u8(sp + i);
-                    continue;
-                }
-                const uint32_t so = static_cast<uint32_t>(sp - rd.base);
+            // len chars from stage offset so to d: bytes up to a 4-byte
+            // boundary of d, dwords up to a 16-byte one, aligned 16-byte
+            // stores, then dwords and bytes
+            auto copy_run = [&](uint8_t* d, uint32_t so, uint32_t len) {
                 const uint32_t head = min<uint32_t>(len, (4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
                 uint32_t i = 0;
 #pragma nounroll
                 for (; i < head; ++i) d[i] = rd.lds[so + i];
-                // from here d + i is 4-aligned: dwords, 16-byte pieces once it is
-                // 16-aligned, dwords, bytes
                 const uint32_t sa = (so + i) & 3;
                 lds_u32c* sw = reinterpret_cast<lds_u32c*>(rd.lds + ((so + i) & ~3u));
                 uint32_t* dw = reinterpret_cast<uint32_t*>(d + i);
-                uint32_t nd = (len - i) >> 2;
+                const uint32_t nd = (len - i) >> 2;
                 uint32_t w0 = sw[0], j = 0;
                 const uint32_t pre = min<uint32_t>(nd, ((16 - (reinterpret_cast<uintptr_t>(dw) & 15)) & 15) >> 2);
 #pragma nounroll
@@ -1687,6 +1679,58 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
                 }
 #pragma nounroll
                 for (i += 4 * nd; i < len; ++i) d[i] = rd.lds[so + i];
+            };
+            // where record k's chars are on the wire
+            auto chars_at = [&](uint32_t k) -> uint64_t {
+                if (L.u.s.src[k] != kFar) return b0 + L.u.s.src[k];
+                uint64_t sp = b0 + L.tbl[k] + a.prefix_len;
+                for (uint32_t g = 0; g < f; ++g) sp += a.size[g] ? a.size[g] : 8 + rd.u64(sp);
+                return sp + 8;
+            };
+            if (ftot >= static_cast<uint64_t>(kWaveCopyAvg) * nw) {
+                // long strings (few records a block): a wave per record, a lane
+                // per aligned 16-byte piece of its chars; its unaligned head and
+                // tail (< 16 bytes each) byte by byte by lanes 0 and 1
+                const uint32_t lane = tid & 63;
+                for (uint32_t k = tid >> 6; k < nw; k += kBlock / 64) {
+                    const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
+                    if (!len) continue;
+                    const uint64_t sp = chars_at(k);
+                    uint8_t* d = chars + P + o;
+                    if (!rd.staged(sp, sp + len)) {
+                        for (uint32_t i = lane; i < len; i += 64) d[i] = rd.u8(sp + i);
+                        continue;
+                    }
+                    const uint32_t so = static_cast<uint32_t>(sp - rd.base);
+                    const uint32_t a0 = min<uint32_t>(len, (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
+                    const uint32_t n16 = (len - a0) >> 4, t0 = a0 + 16 * n16;
+                    if (lane < 2) {  // lane 0 the head, lane 1 the tail (byte stores)
+                        const uint32_t x0 = lane ? t0 : 0, x1 = lane ? len : a0;
+#pragma nounroll
+                        for (uint32_t x = x0; x < x1; ++x) d[x] = rd.lds[so + x];
+                    }
+                    for (uint32_t c = lane; c < n16; c += 64) {
+                        const uint32_t x = so + a0 + 16 * c;
+                        lds_u32c* q = reinterpret_cast<lds_u32c*>(rd.lds + (x & ~3u));
+                        const uint32_t s3 = x & 3, w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+                        *reinterpret_cast<u32x4*>(d + a0 + 16 * c) =
+                            u32x4{__builtin_amdgcn_alignbyte(w1, w0, s3), __builtin_amdgcn_alignbyte(w2, w1, s3),
+                                  __builtin_amdgcn_alignbyte(w3, w2, s3), __builtin_amdgcn_alignbyte(w4, w3, s3)};
+                    }
+                }
+            } else {
+                // lane per record
+                for (uint32_t k = tid; k < nw; k += kBlock) {
+                    const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
+                    if (!len) continue;
+                    const uint64_t sp = chars_at(k);
+                    uint8_t* d = chars + P + o;
+                    if (!rd.staged(sp, sp + len)) {
+                        for (uint32_t i = 0; i < len; ++i) d[i] = rd.u8(sp + i);
+                        continue;
+                    }
+                    copy_run(d, static_cast<uint32_t>(sp - rd.base), len);
+                }
             }
             __syncthreads();
         }

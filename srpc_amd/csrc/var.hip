@@ -1578,6 +1578,8 @@ constexpr uint64_t kLookAgg = 1ull << 62, kLookIncl = 2ull << 62, kLookVal = (1u
 // past it the tile gives up, sets SRPC_STATUS_STALLED and uses what it has --
 // a wrong result that is reported, never a hung GPU.
 constexpr uint32_t kLookSpinMax = 1u << 21;
+// the budget in force (a test hook lowers it to force the STALLED report)
+__device__ uint32_t g_look_spin_max = kLookSpinMax;
 
 __device__ __forceinline__ uint64_t look_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1604,6 +1606,7 @@ __device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2,
     uint64_t pre = 0;
     bool done = false;
     uint32_t spins = 0;
+    const uint32_t spin_max = g_look_spin_max;
     // 1. earlier tiles of the own block, nearest INCL first
     if (q) {
         while (true) {
@@ -1611,7 +1614,7 @@ __device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2,
             const uint64_t incl = __ballot(lane < q && v >= kLookIncl);
             const uint32_t from = incl ? 63 - __builtin_clzll(incl) : 0;  // highest INCL lane, or 0
             const uint64_t wait = __ballot(lane < q && lane >= from && v < kLookAgg);
-            if (wait && ++spins < kLookSpinMax) {
+            if (wait && ++spins < spin_max) {
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
@@ -1635,7 +1638,7 @@ __device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2,
         const uint64_t wait = __ballot(v < kLookAgg);
         const uint32_t first = incl ? __builtin_ctzll(incl) : 64;
         const uint64_t upto = first >= 63 ? ~0ull : (2ull << first) - 1;
-        if ((wait & upto) && ++spins < kLookSpinMax) {
+        if ((wait & upto) && ++spins < spin_max) {
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -2360,6 +2363,14 @@ bool rtu_layout(const srpc_plan* p, uint64_t avg, RtuArgs* out, uint32_t* total)
 using namespace srpc_impl;
 
 extern "C" {
+
+// Test hook (not part of the C ABI in include/): the multi-string unpack's
+// look-back spin budget (0 = the default, 2^21 polls); a tiny budget makes
+// tiles give up and report SRPC_STATUS_STALLED.  Returns SRPC_OK.
+__attribute__((visibility("default"))) int srpc_debug_var_spin_limit(uint32_t spins) {
+    const uint32_t v = spins ? spins : kLookSpinMax;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_look_spin_max), &v, sizeof(v)) == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+}
 
 #ifdef SRPC_PHASES
 int srpc_debug_phases(uint64_t* host8, int reset) {

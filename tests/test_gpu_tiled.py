@@ -126,3 +126,31 @@ def test_pack_then_tiled_unpack_round_trip():
     table, _ = _table_from(p, offs, n)
     back, boffs, st = _unpack_tiled(p, kinds, got, n, rec, table)
     _check(kinds, p, wire, n, back, boffs, st)
+
+
+def test_stalled_look_back_is_reported_and_a_retry_is_exact():
+    """SRPC_STATUS_STALLED (srpc_gpu.h): a multi-string tile whose chars-offset
+    look-back outwaits its budget gives up and says so -- the call returns, the
+    status carries STALLED, and the caller's retry decodes exactly.  The test
+    hook srpc_debug_var_spin_limit shrinks the budget to one poll so tiles give
+    up whenever a predecessor has not published yet."""
+    import ctypes
+
+    from srpc_amd import _lib
+    hook = _lib.lib().srpc_debug_var_spin_limit
+    hook.argtypes, hook.restype = [ctypes.c_uint32], ctypes.c_int
+    kinds, cols, offs, p, wire = _case("two_str", 200_000, 40, True, 3)
+    n = 200_000
+    rec = _rec_offsets(kinds, offs, n, len(p.prefix))
+    assert hook(1) == 0
+    try:
+        back, boffs, st = _unpack_tiled(p, kinds, wire, n, rec, None)
+    finally:
+        assert hook(0) == 0
+    stalled = 4  # SRPC_STATUS_STALLED (include/srpc_gpu.h)
+    flags = st[0]
+    assert flags & ~stalled == 0
+    if not flags & stalled:  # no tile had to wait: the outputs are exact
+        _check(kinds, p, wire, n, back, boffs, st)
+    back, boffs, st = _unpack_tiled(p, kinds, wire, n, rec, None)  # the retry
+    _check(kinds, p, wire, n, back, boffs, st)

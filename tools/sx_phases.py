@@ -79,6 +79,8 @@ def main():
               f"   total {spec.sum(1).mean():8.0f} cycles/block")
         print("  k_sx_decode " + "  ".join(f"{k} {v:8.0f}" for k, v in zip(DEC, dec[ran].mean(0))) +
               f"   total {dec[ran].sum(1).mean():8.0f} cycles/block", flush=True)
+        print(f"  decode fast path (entered at sF, one segment): {b[ran, 15].mean():.3f} of the blocks decoded",
+              flush=True)
 
 
 if __name__ == "__main__":
