@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -681,6 +682,13 @@ const bool g_aos_unstaged = [] {
     return e && e[0] == '1';
 }();
 
+// Whether unpack takes the layout kernels too (SRPC_AOS_LAY_UNPACK=1 at load,
+// or the srpc_debug_aos_lay_unpack test hook).
+std::atomic<bool> g_aos_lay_unpack{[] {
+    const char* e = std::getenv("SRPC_AOS_LAY_UNPACK");
+    return e && e[0] == '1';
+}()};
+
 // A/B switch (SRPC_AOS_NOLAY=1 at load): the staged kernels for the layouts above too.
 const bool g_aos_nolay = [] {
     const char* e = std::getenv("SRPC_AOS_NOLAY");
@@ -752,7 +760,11 @@ static int unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_l
     if (n_fit && !a.ident && !g_aos_unstaged && !(a.fill && g_aos_fill_staged) &&
         launch_aos_run(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
-    if (n_fit && !g_aos_unstaged && !g_aos_nolay &&
+    // the layout kernels' strided whole-struct stores run 0.78 of peak on some
+    // boxes of the pool and 0.41 on others (the staged kernels' coalesced ones
+    // 0.52 on both, profiles/r04_aos_lay_ab.log): unpack takes them only when
+    // asked (SRPC_AOS_LAY_UNPACK=1)
+    if (n_fit && !g_aos_unstaged && !g_aos_nolay && g_aos_lay_unpack.load(std::memory_order_relaxed) &&
         launch_aos_lay(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
     if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
@@ -785,6 +797,12 @@ int srpc_gpu_unpack_aos_fill(const srpc_plan* p, const uint8_t* d_wire, uint64_t
                              const void* h_fill, srpc_unpack_status* d_status, void* stream) {
     if (!h_fill) return SRPC_E_INVALID;
     return unpack_aos(p, d_wire, wire_len, n, d_records, record_stride, field_offsets, h_fill, d_status, stream);
+}
+
+// Test hook (not part of the C ABI in include/): 1 = unpack takes the layout
+// kernels too, 0 = the staged ones; returns the previous setting.
+__attribute__((visibility("default"))) int srpc_debug_aos_lay_unpack(int on) {
+    return g_aos_lay_unpack.exchange(on != 0) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -272,32 +272,6 @@ template <int S>
 __device__ __forceinline__ uint4 gather_chunk(const uint8_t* img, uint32_t e0, uint32_t ne,
                                               uint32_t stride, uint32_t off) {
     uint4 q = make_uint4(0, 0, 0, 0);
-#ifndef SRPC_TILE_GATHER_OLD
-    if constexpr (S >= 2) {
-        // elements at any byte offset from aligned dword reads and byte funnel
-        // shifts (a misaligned ds_read costs ~6x an aligned one,
-        // profiles/r01_lds_unaligned.log); the reads may touch up to 4 bytes
-        // past the element, inside the LDS allocation (template / mask follow)
-        uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 16 / S; ++j) {
-            if (static_cast<uint32_t>(j) >= ne) break;
-            const uint32_t x = (e0 + j) * stride + off;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(img + (x & ~3u));
-            const uint32_t sh = x & 3;
-            if constexpr (S == 8) {
-                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-                o[2 * j] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                o[2 * j + 1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            } else {
-                const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-                if constexpr (S == 4) o[j] = v;
-                else o[j >> 1] |= (v & 0xffffu) << (16 * (j & 1));
-            }
-        }
-        return make_uint4(o[0], o[1], o[2], o[3]);
-    }
-#endif
     uint8_t* b = reinterpret_cast<uint8_t*>(&q);
 #pragma unroll
     for (int j = 0; j < 16 / S; ++j)
@@ -706,11 +680,6 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
         const uint32_t tbytes = nr * a.stride;
         const uint32_t full = tbytes >> 4;
         // kLoadBatch independent 16-byte loads in flight per lane before any is used
-#ifndef SRPC_TILE_GATHER_OLD
-        // the template phase of chunk c, stepped instead of divided per chunk
-        const uint32_t step = a.prefix_len ? (16 * kBlock) % a.L : 0;
-        uint32_t ph_run = a.prefix_len ? (16 * threadIdx.x) % a.L : 0;
-#endif
         for (uint32_t c0 = threadIdx.x; c0 < full; c0 += kBlock * kLoadBatch) {
             uint4 vv[kLoadBatch];
 #pragma unroll
@@ -723,17 +692,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_tile(TileArgs a, const uint8_
                 const uint32_t c = c0 + u * kBlock;
                 if (c >= full) break;
                 const uint4 v = vv[u];
-#ifndef SRPC_TILE_GATHER_OLD
-                const uint32_t ph_c = ph_run;
-                ph_run += step;
-                if (ph_run >= a.L) ph_run -= a.L;
-#endif
                 if (a.prefix_len && st) {
-#ifndef SRPC_TILE_GATHER_OLD
-                    const uint32_t ph = ph_c;
-#else
                     const uint32_t ph = (16 * c) % a.L;
-#endif
                     const uint4 m = *reinterpret_cast<const uint4*>(mask + ph);
                     const uint4 t = *reinterpret_cast<const uint4*>(tmpl + ph);
                     const uint32_t d0 = (v.x & m.x) ^ t.x, d1 = (v.y & m.y) ^ t.y;

@@ -217,3 +217,57 @@ def test_aos_errors():
     st = status_buf()
     pr.unpack_aos(dev(np.frombuffer(bytes(wb), np.uint8)), len(wb), 100, back, stride, offs, st)
     assert read_status(st) == (srpc_amd.SRPC_STATUS_PREFIX, 42)
+
+
+@pytest.fixture(params=["staged_unpack", "layout_unpack"])
+def lay_unpack(request):
+    """srpc_debug_aos_lay_unpack: the all-kinds struct's unpack through the
+    compile-time layout kernels too (off by default: their strided
+    whole-struct stores are box-dependent)."""
+    import ctypes
+
+    from srpc_amd import _lib
+    hook = _lib.lib().srpc_debug_aos_lay_unpack
+    hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
+    prev = hook(1 if request.param == "layout_unpack" else 0)
+    yield request.param
+    hook(prev)
+
+
+@pytest.mark.parametrize("n", [1, 17, 255, 256, 257, 4099, 100_003])
+@pytest.mark.parametrize("vptr", [True, False])
+def test_aos_all_kinds_layout_kernels_both_unpacks(n, vptr, lay_unpack):
+    """The all-kinds struct (with and without the vtable slot) in place and
+    into fresh objects, by either unpack kernel family, against the oracle."""
+    kinds = [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64]
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker(sch)
+    rng = np.random.default_rng(17 * n + vptr)
+    recs = random_records(kinds, n, rng, vptr)
+    stride, offs = layout(recs, len(kinds))
+    cols = [np.ascontiguousarray(recs[f"f{i}"]) for i in range(len(kinds))]
+    want = bytes(oracle.pack(kinds, cols, n, p.prefix))
+    other = random_records(kinds, n, np.random.default_rng(3 + n), vptr)
+    d_other = dev(other.view(np.uint8).reshape(-1).copy())
+    st = status_buf()
+    assert p.unpack_aos(dev(np.frombuffer(want, np.uint8)), len(want), n, d_other, stride, offs, st) == 0
+    assert read_status(st) == (0, 2**64 - 1)
+    back = host(d_other, n * stride).view(recs.dtype)
+    for i in range(len(kinds)):
+        assert back[f"f{i}"].tobytes() == recs[f"f{i}"].tobytes(), i
+    mask = np.zeros(stride, bool)
+    mask[0:8 if vptr else 0] = True
+    for o, k in zip(offs, kinds):
+        mask[o:o + oracle.KIND_SIZE[k]] = True
+    pad = np.flatnonzero(~mask)
+    assert np.array_equal(back.view(np.uint8).reshape(n, stride)[:, pad],
+                          other.view(np.uint8).reshape(n, stride)[:, pad])
+    fill = rng.integers(0, 256, stride, dtype=np.uint8).tobytes()
+    d_fresh = dev(other.view(np.uint8).reshape(-1).copy())
+    assert p.unpack_aos_fill(dev(np.frombuffer(want, np.uint8)), len(want), n, d_fresh, stride, offs, fill, st) == 0
+    assert read_status(st) == (0, 2**64 - 1)
+    got = host(d_fresh, n * stride).view(np.uint8).reshape(n, stride)
+    expect = np.tile(np.frombuffer(fill, np.uint8), (n, 1))
+    for o, k in zip(offs, kinds):
+        expect[:, o:o + oracle.KIND_SIZE[k]] = recs.view(np.uint8).reshape(n, stride)[:, o:o + oracle.KIND_SIZE[k]]
+    assert np.array_equal(got, expect)
