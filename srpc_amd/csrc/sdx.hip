@@ -109,10 +109,15 @@ __device__ unsigned long long g_sxph_blocks = 0;
     do {                                                                                           \
         if (threadIdx.x == 0 && blockIdx.x < g_sxph_blocks) g_sxph[static_cast<uint64_t>(blockIdx.x) * 16 + (i)] = 1; \
     } while (0)
+#define SXP_SET(i, v)                                                                              \
+    do {                                                                                           \
+        if (blockIdx.x < g_sxph_blocks) g_sxph[static_cast<uint64_t>(blockIdx.x) * 16 + (i)] = (v);    \
+    } while (0)
 #else
 #define SXP_BEGIN
 #define SXP(i)
 #define SXP_FLAG(i)
+#define SXP_SET(i, v)
 #endif
 
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
@@ -981,6 +986,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
             if (C.tail[k]) lastc = 64 * k + 63 - __builtin_clzll(C.tail[k]);
         }
         const bool one = sF != ~0ull && ntail == 1 && (C.stop[lastc] || C.exit[lastc] >= b1);
+        SXP_SET(14, ntail);
         uint64_t* h = S.hdr + 4 * b;
         h[0] = wmask;
         h[1] = sF;

@@ -81,6 +81,9 @@ def main():
               f"   total {dec[ran].sum(1).mean():8.0f} cycles/block", flush=True)
         print(f"  decode fast path (entered at sF, one segment): {b[ran, 15].mean():.3f} of the blocks decoded",
               flush=True)
+        nt = b[:, 14]
+        print(f"  speculation segments per block: mean {nt.mean():.2f}, one {np.mean(nt == 1):.3f}, "
+              f"two {np.mean(nt == 2):.3f}, more {np.mean(nt > 2):.3f}", flush=True)
 
 
 if __name__ == "__main__":
