@@ -222,6 +222,77 @@ __global__ __launch_bounds__(kBlock) void k_unpack_aos_run_fill(const uint8_t* _
         d[k] = static_cast<uint64_t>(a.fillw[2 * k]) | (static_cast<uint64_t>(a.fillw[2 * k + 1]) << 32);
 }
 
+// k_unpack_aos_run(_fill) with whole-line stores: a wave per 256 structs,
+// the wire tile in LDS; lane c writes bytes [16c, 16c + 16) of the tile's
+// structs (every store instruction covers 1 KiB of the array contiguously),
+// each dword from the run (the LDS tile) or, outside it, from the fill record
+// (fresh objects) or the array itself (in place: a coalesced load of the
+// piece when it has such a dword).  Struct stride and run offset multiples of
+// 8, the array 16-byte aligned.
+template <uint32_t W, bool kFill>
+__global__ __launch_bounds__(64, 8) void k_unpack_aos_run_piece(const uint8_t* __restrict__ wire,
+                                                                uint8_t* __restrict__ recs, AosArgs a, uint64_t n) {
+    constexpr uint32_t TR = 256;
+    __shared__ __attribute__((aligned(16))) uint32_t img[TR * W / 4];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * TR;
+    const uint32_t nr = static_cast<uint32_t>(min<uint64_t>(TR, n - t0));
+    const uint32_t wbytes = nr * W;  // a multiple of 8
+    const v4u* src = reinterpret_cast<const v4u*>(wire + t0 * W);
+    for (uint32_t c = lane; c < wbytes / 16; c += 64) reinterpret_cast<v4u*>(img)[c] = __builtin_nontemporal_load(src + c);
+    if (wbytes & 8 && lane == 0)
+        reinterpret_cast<uint64_t*>(img)[wbytes / 8 - 1] = reinterpret_cast<const uint64_t*>(wire + t0 * W)[wbytes / 8 - 1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes before its reads
+    const uint32_t rs = a.rstride, boff = static_cast<uint32_t>(a.boff);
+    const uint32_t obytes = nr * rs;  // a multiple of 8
+    v4u* out = reinterpret_cast<v4u*>(recs + t0 * rs);
+    for (uint32_t c = lane; 16 * c < obytes; c += 64) {
+        const uint32_t gb = 16 * c;
+        uint32_t sidx = gb / rs, ob = gb - sidx * rs;
+        uint32_t o[4];
+        bool need_old = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const bool in_run = ob >= boff && ob < boff + W;
+            o[d] = in_run ? img[(sidx * W + ob - boff) >> 2] : a.fillw[ob >> 2];
+            need_old |= !in_run;
+            ob += 4;
+            if (ob == rs) {
+                ob = 0;
+                ++sidx;
+            }
+        }
+        const bool whole = gb + 16 <= obytes;
+        if constexpr (!kFill) {
+            if (need_old) {  // the dwords outside the run as they are
+                uint32_t od[4];
+                if (whole) {
+                    const v4u v = out[c];
+                    od[0] = v.x, od[1] = v.y, od[2] = v.z, od[3] = v.w;
+                } else {
+                    od[0] = reinterpret_cast<const uint32_t*>(out + c)[0];
+                    od[1] = reinterpret_cast<const uint32_t*>(out + c)[1];
+                    od[2] = od[3] = 0;
+                }
+                uint32_t ob2 = gb - (gb / rs) * rs;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    if (!(ob2 >= boff && ob2 < boff + W)) o[d] = od[d];
+                    ob2 += 4;
+                    if (ob2 == rs) ob2 = 0;
+                }
+            }
+        }
+        if (whole) {
+            out[c] = v4u{o[0], o[1], o[2], o[3]};
+        } else {  // the array's last 8 bytes
+            reinterpret_cast<uint32_t*>(out + c)[0] = o[0];
+            reinterpret_cast<uint32_t*>(out + c)[1] = o[1];
+        }
+    }
+}
+
 // The fill record into every struct of [0, n) (the per-field fallback's first
 // pass when unpacking into fresh objects): a lane per 4 bytes, or per byte.
 __global__ __launch_bounds__(kBlock) void k_aos_fill(uint8_t* __restrict__ recs, AosArgs a, uint64_t n) {
@@ -239,6 +310,13 @@ __global__ __launch_bounds__(kBlock) void k_aos_fill(uint8_t* __restrict__ recs,
     }
 }
 
+// A/B switch (SRPC_AOS_RUN_PIECE=0 at load): the run kernels' unpack without
+// the piece kernel.
+const bool g_aos_run_piece = [] {
+    const char* e = std::getenv("SRPC_AOS_RUN_PIECE");
+    return !(e && e[0] == '0');
+}();
+
 // The run kernels for wire bodies of 8, 16, 24 or 32 bytes (8-byte aligned
 // struct array, stride and body offset), else false.
 bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
@@ -248,10 +326,18 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
     const uint64_t g = (n + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return false;
     const uint32_t boff = static_cast<uint32_t>(a.boff);
+    // unpack: whole-line piece stores when the array is 16-byte aligned and
+    // the struct fits the fill record (the run kernels' strided stores: 0.65
+    // into fresh objects, profiles/r04z_aos_piece_ab.log)
+    const uint64_t gpn = (n + 255) / 256;
+    const bool pieces = !pack && g_aos_run_piece && aligned(dst, 16) && a.rstride <= kAosFillMax && gpn <= 0x7fffffffull;
+    const dim3 gp(static_cast<uint32_t>(gpn));
 #define SRPC_AOS_RUN(Wb)                                                                                         \
     if (a.wstride == Wb) {                                                                                       \
         if (pack) launch(k_pack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, a.rstride, \
                          boff, dst, n);                                                                          \
+        else if (pieces && a.fill) launch(k_unpack_aos_run_piece<Wb, true>, gp, dim3(64), 0, s, src, dst, a, n);  \
+        else if (pieces) launch(k_unpack_aos_run_piece<Wb, false>, gp, dim3(64), 0, s, src, dst, a, n);           \
         else if (a.fill) launch(k_unpack_aos_run_fill<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s,  \
                                 src, dst, a, n);                                                         \
         else launch(k_unpack_aos_run<Wb>, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, src, dst,         \
@@ -457,24 +543,131 @@ bool aos_lay_match(const AosArgs& a) {
     return true;
 }
 
+// Unpack with whole-line stores (struct sizes a multiple of 16 bytes, P =
+// RS / 16 pieces per struct): lane c of the wave writes bytes [16c, 16c + 16)
+// of the tile's structs, so every store instruction covers 1 KiB of the array
+// contiguously and no line is written in parts by several instructions.  The
+// lane assembles its piece (half H of struct c / P) from the wire tile in LDS:
+// the record bytes [lo, hi) the piece's fields come from, funnel-shifted from
+// dwords; struct bytes no field covers come from the fill record (fresh
+// objects) or from the struct as it is (in place: a coalesced load of the
+// same piece).
+template <class L, int H>
+struct AosPiece {
+    using T = AosT<L>;
+    static constexpr int lo = [] {
+        int m = T::WS;
+        for (int ob = 16 * H; ob < 16 * H + 16; ++ob) {
+            const int f = T::rfield(ob);
+            if (f >= 0 && T::woff(f) + (ob - L::ROFF[f]) < m) m = T::woff(f) + (ob - L::ROFF[f]);
+        }
+        return m == T::WS ? 0 : m;
+    }();
+    static constexpr int hi = [] {
+        int m = 0;
+        for (int ob = 16 * H; ob < 16 * H + 16; ++ob) {
+            const int f = T::rfield(ob);
+            if (f >= 0 && T::woff(f) + (ob - L::ROFF[f]) + 1 > m) m = T::woff(f) + (ob - L::ROFF[f]) + 1;
+        }
+        return m;
+    }();
+    static constexpr int ND = hi > lo ? (hi - lo + 3) / 4 : 1;  // record dwords the piece reads
+};
+
+template <class L, int H, bool kFill>
+__device__ __forceinline__ v4u aos_piece(const uint32_t* img, uint32_t srec, const v4u& old, const AosArgs& a) {
+    using T = AosT<L>;
+    using PC = AosPiece<L, H>;
+    const uint32_t at = srec * T::WS + PC::lo, base = at >> 2, sh = at & 3;
+    uint32_t raw[PC::ND + 1];
+#pragma unroll
+    for (int j = 0; j <= PC::ND; ++j) raw[j] = img[base + j];
+    uint32_t w[PC::ND];
+#pragma unroll
+    for (int j = 0; j < PC::ND; ++j) w[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], sh);
+    const uint32_t od[4] = {old.x, old.y, old.z, old.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ob = 16 * H + 4 * d + i, f = T::rfield(ob);
+            uint32_t byte;
+            if (f >= 0) byte = aos_byte(w, T::woff(f) + (ob - L::ROFF[f]) - PC::lo);
+            else if (kFill) byte = (a.fillw[ob >> 2] >> (8 * (ob & 3))) & 0xffu;
+            else byte = (od[d] >> (8 * i)) & 0xffu;
+            v |= byte << (8 * i);
+        }
+        o[d] = v;
+    }
+    return v4u{o[0], o[1], o[2], o[3]};
+}
+
+template <class L, bool kFill>
+__global__ __launch_bounds__(kAosWave, 8) void k_unpack_aos_piece(const uint8_t* __restrict__ wire,
+                                                                  uint8_t* __restrict__ recs, uint64_t n, AosArgs a) {
+    using T = AosT<L>;
+    constexpr int G = kAosLayG, WD = G * T::WS / 4, TR = kAosWave * G, P = L::RS / 16;
+    static_assert(L::RS % 16 == 0 && (P == 1 || P == 2), "structs of 16 or 32 bytes");
+    __shared__ __attribute__((aligned(16))) uint32_t img[kAosWave * WD + 8];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * TR;
+    const uint64_t nr = min<uint64_t>(TR, n - t0);
+    const uint32_t bytes = static_cast<uint32_t>(nr) * T::WS, full = bytes >> 4;
+    const uint8_t* src = wire + t0 * T::WS;
+    for (uint32_t c = lane; c < full; c += kAosWave)
+        reinterpret_cast<v4u*>(img)[c] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + c);
+    for (uint32_t i = 16 * full + lane; i < bytes; i += kAosWave) reinterpret_cast<uint8_t*>(img)[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes before its reads
+    v4u* out = reinterpret_cast<v4u*>(recs + t0 * L::RS);
+    const uint32_t npieces = static_cast<uint32_t>(nr) * P;
+#pragma unroll
+    for (int k = 0; k < TR * P / kAosWave; ++k) {
+        const uint32_t c = lane + kAosWave * k;
+        if (c >= npieces) break;
+        v4u old{0, 0, 0, 0};
+        if constexpr (!kFill) old = out[c];
+        v4u v;
+        if constexpr (P == 1) v = aos_piece<L, 0, kFill>(img, c, old, a);
+        else v = (lane & 1) ? aos_piece<L, 1, kFill>(img, c >> 1, old, a) : aos_piece<L, 0, kFill>(img, c >> 1, old, a);
+        out[c] = v;
+    }
+}
+
 // The layout kernels for a struct array that matches one (16-byte aligned
-// array and wire), else false.
+// array and wire), else false.  Unpack: umode 1 takes the per-lane struct
+// kernel, umode 2 the whole-line piece kernel where the struct size allows it
+// (else false: the staged kernels).
 template <class L>
-bool launch_aos_lay1(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+bool launch_aos_lay1(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s,
+                     int umode) {
     if (!aos_lay_match<L>(a)) return false;
     const uint64_t g = (n + kAosWave * kAosLayG - 1) / (kAosWave * kAosLayG);
     if (g > 0x7fffffffull) return false;
     const dim3 grid(static_cast<uint32_t>(g));
+    constexpr bool kPieces = L::RS == 16 || L::RS == 32;
+    if constexpr (!kPieces) {
+        if (!pack && umode == 2) return false;  // the staged kernels (coalesced stores)
+    } else {
+        if (!pack && umode == 2) {
+            if (a.fill) launch(k_unpack_aos_piece<L, true>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
+            else launch(k_unpack_aos_piece<L, false>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
+            return true;
+        }
+    }
     if (pack) launch(k_pack_aos_lay<L>, grid, dim3(kAosWave), 0, s, src, dst, n);
     else if (a.fill) launch(k_unpack_aos_lay<L, true>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
     else launch(k_unpack_aos_lay<L, false>, grid, dim3(kAosWave), 0, s, src, dst, n, a);
     return true;
 }
 
-bool launch_aos_lay(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+bool launch_aos_lay(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s,
+                    int umode = 0) {
     if (!aligned(src, 16) || !aligned(dst, 16)) return false;
-    return launch_aos_lay1<AosLayAllKindsV>(a, pack, src, dst, n, s) ||
-           launch_aos_lay1<AosLayAllKinds>(a, pack, src, dst, n, s);
+    return launch_aos_lay1<AosLayAllKindsV>(a, pack, src, dst, n, s, umode) ||
+           launch_aos_lay1<AosLayAllKinds>(a, pack, src, dst, n, s, umode);
 }
 
 // HBM bytes [0, bytes) of a tile -> LDS (16-byte pieces, then single bytes).
@@ -682,11 +875,12 @@ const bool g_aos_unstaged = [] {
     return e && e[0] == '1';
 }();
 
-// Whether unpack takes the layout kernels too (SRPC_AOS_LAY_UNPACK=1 at load,
-// or the srpc_debug_aos_lay_unpack test hook).
-std::atomic<bool> g_aos_lay_unpack{[] {
+// Which kernels unpack takes for the layouts above (SRPC_AOS_LAY_UNPACK=N at
+// load, or the srpc_debug_aos_lay_unpack test hook): 0 the staged ones, 1 the
+// per-lane struct kernel, 2 (default) the whole-line piece kernel.
+std::atomic<int> g_aos_lay_unpack{[] {
     const char* e = std::getenv("SRPC_AOS_LAY_UNPACK");
-    return e && e[0] == '1';
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
 }()};
 
 // A/B switch (SRPC_AOS_NOLAY=1 at load): the staged kernels for the layouts above too.
@@ -760,12 +954,13 @@ static int unpack_aos(const srpc_plan* p, const uint8_t* d_wire, uint64_t wire_l
     if (n_fit && !a.ident && !g_aos_unstaged && !(a.fill && g_aos_fill_staged) &&
         launch_aos_run(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
-    // the layout kernels' strided whole-struct stores run 0.78 of peak on some
-    // boxes of the pool and 0.41 on others (the staged kernels' coalesced ones
-    // 0.52 on both, profiles/r04_aos_lay_ab.log): unpack takes them only when
-    // asked (SRPC_AOS_LAY_UNPACK=1)
-    if (n_fit && !g_aos_unstaged && !g_aos_nolay && g_aos_lay_unpack.load(std::memory_order_relaxed) &&
-        launch_aos_lay(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s))
+    // the layout kernels: the 32-byte struct a lane per 16-byte piece
+    // (whole-line stores: 0.69 into fresh objects where the lane-per-struct
+    // kernel's strided stores run 0.41 and the staged kernels 0.55,
+    // profiles/r04z_aos_piece_ab.log); the 24-byte one takes the staged kernels
+    const int umode = g_aos_lay_unpack.load(std::memory_order_relaxed);
+    if (n_fit && !g_aos_unstaged && !g_aos_nolay && umode &&
+        launch_aos_lay(a, false, d_wire, static_cast<uint8_t*>(d_records), n_fit, s, umode))
         return hipGetLastError() == hipSuccess ? ret : SRPC_E_HIP;
     if (n_fit && aligned(d_records, 16) && !g_aos_unstaged) {
         const uint32_t lds = staged_tiling(&a);
@@ -799,10 +994,11 @@ int srpc_gpu_unpack_aos_fill(const srpc_plan* p, const uint8_t* d_wire, uint64_t
     return unpack_aos(p, d_wire, wire_len, n, d_records, record_stride, field_offsets, h_fill, d_status, stream);
 }
 
-// Test hook (not part of the C ABI in include/): 1 = unpack takes the layout
-// kernels too, 0 = the staged ones; returns the previous setting.
-__attribute__((visibility("default"))) int srpc_debug_aos_lay_unpack(int on) {
-    return g_aos_lay_unpack.exchange(on != 0) ? 1 : 0;
+// Test hook (not part of the C ABI in include/): which kernels unpack takes
+// for the layout-kernel structs (0 staged, 1 per-lane structs, 2 whole-line
+// pieces); returns the previous setting.
+__attribute__((visibility("default"))) int srpc_debug_aos_lay_unpack(int mode) {
+    return g_aos_lay_unpack.exchange(mode < 0 ? 0 : mode > 2 ? 2 : mode);
 }
 
 }  // extern "C"

@@ -63,10 +63,14 @@ def layout(recs, nfields):
     # compile-time layout kernels (aos.hip k_*_aos_lay; n = 1..100003 covers
     # the array's last, partial lane)
     ("all", None, False, 0),
+    # runs of 8 / 24 / 32 bytes behind a vtable slot (structs of 16 / 32 /
+    # 40 bytes): the run kernels, whole-line piece unpack
+    ("pair", None, True, 0), ("i64x3", None, True, 0), ("i64x4", None, True, 0),
     # a struct array 8 bytes off 16-byte alignment: the per-field kernels
     ("quad", None, True, 8), ("all", "request", True, 8)])
 def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
-    kinds = {"quad": [oracle.INT32] * 4,
+    kinds = {"quad": [oracle.INT32] * 4, "pair": [oracle.INT32] * 2, "i64x3": [oracle.INT64] * 3,
+             "i64x4": [oracle.INT64] * 4,
              "all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
              "number": [oracle.INT32], "i64_i8": [oracle.INT64, oracle.INT8],
              "wide": [oracle.INT8, oracle.INT64, oracle.INT16, oracle.INT8, oracle.INT32] * 3}[schema]
@@ -112,15 +116,17 @@ def test_aos_pack_unpack_vs_oracle(n, schema, envelope, vptr, shift):
 
 @pytest.mark.parametrize("n", [1, 17, 4099, 100_003])
 @pytest.mark.parametrize("schema,envelope,vptr,shift", [
-    ("quad", None, True, 0),          # the run kernel (fields one run behind the vtable slot)
-    ("all", None, True, 0), ("all", None, False, 0),  # layout kernels (k_unpack_aos_lay<L, true>)
+    ("quad", None, True, 0),          # the run kernels (fields one run behind the vtable slot)
+    ("pair", None, True, 0), ("i64x3", None, True, 0), ("i64x4", None, True, 0),
+    ("all", None, True, 0), ("all", None, False, 0),  # layout kernels
     ("all", "request", True, 0), ("i64_i8", None, True, 0),  # staged kernels
     ("quad", None, False, 0),         # fields cover the struct: no fill needed
     ("quad", None, True, 8), ("all", "request", True, 8)])  # per-field kernels (+ a fill pass)
 def test_aos_unpack_into_fresh_objects(n, schema, envelope, vptr, shift):
     """srpc_gpu_unpack_aos_fill: the leaf fields from the wire, every other
     struct byte from the fill record (a T{} image), whatever the array held."""
-    kinds = {"quad": [oracle.INT32] * 4,
+    kinds = {"quad": [oracle.INT32] * 4, "pair": [oracle.INT32] * 2, "i64x3": [oracle.INT64] * 3,
+             "i64x4": [oracle.INT64] * 4,
              "all": [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64],
              "i64_i8": [oracle.INT64, oracle.INT8]}[schema]
     sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
@@ -219,17 +225,22 @@ def test_aos_errors():
     assert read_status(st) == (srpc_amd.SRPC_STATUS_PREFIX, 42)
 
 
-@pytest.fixture(params=["staged_unpack", "layout_unpack"])
+LAY_UNPACK = {"staged_unpack": 0, "layout_unpack": 1, "piece_unpack": 2}
+
+
+@pytest.fixture(params=list(LAY_UNPACK))
 def lay_unpack(request):
     """srpc_debug_aos_lay_unpack: the all-kinds struct's unpack through the
-    compile-time layout kernels too (off by default: their strided
-    whole-struct stores are box-dependent)."""
+    staged kernels, the compile-time layout kernel with a lane per four
+    structs, or the layout kernel with a lane per 16-byte piece of the
+    structs (whole-line stores, the default; the 24-byte struct falls back
+    to the staged kernels), DESIGN.md §4.5."""
     import ctypes
 
     from srpc_amd import _lib
     hook = _lib.lib().srpc_debug_aos_lay_unpack
     hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_int
-    prev = hook(1 if request.param == "layout_unpack" else 0)
+    prev = hook(LAY_UNPACK[request.param])
     yield request.param
     hook(prev)
 

@@ -20,7 +20,7 @@ LABELS = {
     "two_numbers_response_23B_16M": ("TwoNumbers response 23 B", "TILE / rec unpack"),
     "quad_aos_16M": ("Quad as 24-B structs (vtable slot)", "AoS run"),
     "quad_aos_plain_16M": ("Quad as plain 16-B structs", "AoS tile copy"),
-    "all_kinds_aos_16M": ("all 6 kinds as 32-B structs (vtable slot)", "AoS layout pack / staged unpack"),
+    "all_kinds_aos_16M": ("all 6 kinds as 32-B structs (vtable slot)", "AoS layout pack / piece unpack"),
     "multiple_primitives_str0-64_4M": ("multiple_primitives, strings 0-64 B, 4M", "VAR"),
     "string_0-1024_1M": ("one string 0-1024 B, 1M", "VAR"),
     "string_0-16_8M": ("one string 0-16 B, 8M", "VAR"),
