@@ -225,6 +225,33 @@ def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int =
     out["pipelined"].update({"chunks": chunks, "records_per_chunk": per, "ring_depth": depth,
                              "streams": "H2D / kernels / D2H"})
 
+    # -- native pipeline (ABI 7: srpc_gpu_pack_host / srpc_gpu_unpack_host): the
+    # same chunked ring enqueued by the library, a few HIP calls per chunk
+    h_cols_p = [h.data_ptr() for h in hcols]
+    h_back_p = [h.data_ptr() for h in hback]
+    native = {}
+    for nchunks, ndepth, nstreams in ((16, 3, 3), (16, 3, 2), (0, 1, 3)):
+        os.environ["SRPC_HOST_STREAMS"] = str(nstreams)  # host.hip A/B: kernels on their own stream or the H2D one
+        per_n = n // nchunks if nchunks else 0  # 0: direct, the kernels on the mapped pinned buffers
+        sb = p.host_scratch_bytes(per_n, ndepth)
+        scr = torch.empty(sb + 256, dtype=torch.uint8, device=dev)
+        sp = scr.data_ptr() + (-scr.data_ptr()) % 256
+        hwire.zero_()
+        ms_p = timed(lambda: p.pack_host(h_cols_p, n, hwire, per_n, sp, sb, depth=ndepth, stream=main))
+        okp = torch.equal(hwire, want_wire)
+        for h in hback:
+            h.zero_()
+        ms_u = timed(lambda: p.unpack_host(hwire, n * rb, n, h_back_p, per_n, sp, sb, depth=ndepth, stream=main))
+        oku = all(torch.equal(a, b) for a, b in zip(hback, hcols))
+        ok_pack, ok_unpack = ok_pack and okp, ok_unpack and oku
+        name = f"{nchunks}x{ndepth}_{nstreams}streams" if nchunks else "direct"
+        native[name] = {"pack": leg(ms_p, moved), "unpack": leg(ms_u, moved)}
+        del scr
+    os.environ.pop("SRPC_HOST_STREAMS", None)
+    best = {d: min(native, key=lambda k: native[k][d]["ms"]) for d in ("pack", "unpack")}
+    out["pipelined_native"] = {"configs": native, "best": best,
+                               "what": "chunks x ring depth, enqueued by srpc_gpu_pack_host / _unpack_host"}
+
     # -- the link alone: H2D 256 MiB, D2H 256 MiB, then both at once on two streams
     def h2d():
         with torch.cuda.stream(s_in):
@@ -260,6 +287,9 @@ def pcie_inclusive(p, n: int, dev, reps: int = 3, chunks: int = 16, depth: int =
                                     for d in ("pack", "unpack")}
     out["pipelined_over_duplex_floor"] = {d: round(t_both / out["pipelined"][d]["ms"], 3)
                                           for d in ("pack", "unpack")}
+    nat = {d: out["pipelined_native"]["configs"][best[d]][d]["ms"] for d in ("pack", "unpack")}
+    out["native_over_serial"] = {d: round(out["serial"][d]["ms"] / nat[d], 3) for d in ("pack", "unpack")}
+    out["native_over_duplex_floor"] = {d: round(t_both / nat[d], 3) for d in ("pack", "unpack")}
     out["verified"] = bool(ok_pack and ok_unpack)
     del cols, back, wire, w2, rcols, rwire
     return out

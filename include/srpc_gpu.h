@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 6
+#define SRPC_GPU_ABI_VERSION 7
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -424,6 +424,26 @@ int srpc_frames_offsets(const srpc_plan* const* req_plans, const uint32_t* resp_
  * from state `seed`.  Used by bench.py to build inputs in HBM. */
 int srpc_gpu_fill_splitmix_i32(int32_t* const* d_cols, uint32_t nfields, uint64_t n,
                                uint64_t seed, uint64_t first_record, void* stream);
+
+/* Host-terminated pack / unpack (ABI 7): columns and wire bytes in HOST
+ * memory (pinned for overlap), as the reference's batches start and end --
+ * the packer's byte vector written to the socket (transport.hpp:94-123) and
+ * the received bytes the generated unpack reads (calculator_srpc.cpp:19-22).
+ * A fixed-width batch moves in chunks of `chunk_records` through a ring of
+ * `depth` device buffers carved from d_scratch (256-byte aligned, at least
+ * srpc_plan_host_scratch_bytes), pipelined over internal streams (H2D /
+ * kernels / D2H), ordered after the work on `stream` and before what is
+ * enqueued on it later.  The results equal srpc_gpu_pack / srpc_gpu_unpack
+ * on the whole batch, statuses included (first_bad_record is batch-relative).
+ * String schemas: SRPC_E_UNSUPPORTED. */
+int srpc_plan_host_scratch_bytes(const srpc_plan* plan, uint64_t chunk_records, uint32_t depth,
+                                 uint64_t* out);
+int srpc_gpu_pack_host(const srpc_plan* plan, const void* const* h_cols, uint64_t n, uint8_t* h_wire,
+                       uint64_t wire_cap, uint64_t chunk_records, uint32_t depth, void* d_scratch,
+                       uint64_t scratch_bytes, void* stream);
+int srpc_gpu_unpack_host(const srpc_plan* plan, const uint8_t* h_wire, uint64_t wire_len, uint64_t n,
+                         void* const* h_cols, uint64_t chunk_records, uint32_t depth, void* d_scratch,
+                         uint64_t scratch_bytes, srpc_unpack_status* d_status, void* stream);
 
 /* Measurement hook (bench.py): the data-path kernels launched by the NEXT
  * srpc_gpu_pack / _unpack / _pack_var / _unpack_var call made on this host

@@ -57,6 +57,9 @@ SIGNATURES = {
     "srpc_gpu_unpack_var_tiled": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "srpc_plan_var_stream_scratch_bytes": (C.c_int, [_vp, _u64, _u64, C.POINTER(_u64)]),
     "srpc_gpu_unpack_var_stream": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
+    "srpc_plan_host_scratch_bytes": (C.c_int, [_vp, _u64, C.c_uint32, C.POINTER(_u64)]),
+    "srpc_gpu_pack_host": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _u64, C.c_uint32, _vp, _u64, _vp]),
+    "srpc_gpu_unpack_host": (C.c_int, [_vp, _vp, _u64, _u64, _vp, _u64, C.c_uint32, _vp, _u64, _vp, _vp]),
     "srpc_shard_range": (C.c_int, [_u64, C.c_int, C.c_int, C.POINTER(_u64), C.POINTER(_u64)]),
     "srpc_comm_unique_id": (C.c_int, [_vp]),
     "srpc_comm_init_rank": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),

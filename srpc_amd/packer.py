@@ -174,6 +174,33 @@ class GpuPacker:
                                                 _dptr(status), _stream(stream)),
                      "srpc_gpu_unpack")
 
+    # -- host-terminated batches (ABI 7) ---------------------------------------
+    def host_scratch_bytes(self, chunk_records: int, depth: int = 3) -> int:
+        out = C.c_uint64()
+        check(_lib.lib().srpc_plan_host_scratch_bytes(self._h, chunk_records, depth, C.byref(out)),
+              "srpc_plan_host_scratch_bytes")
+        return out.value
+
+    def pack_host(self, h_cols: Sequence, n: int, h_wire, chunk_records: int, scratch, scratch_bytes: int,
+                  depth: int = 3, wire_cap: int | None = None, stream=None) -> int:
+        """Pack n records from HOST columns into HOST wire bytes, pipelined
+        through `depth` device buffers of `chunk_records` (async on `stream`;
+        host buffers: pinned tensors or addresses)."""
+        arr = self._cols(h_cols)
+        cap = self.wire_bytes(n) if wire_cap is None else wire_cap
+        check(_lib.lib().srpc_gpu_pack_host(self._h, arr, n, _dptr(h_wire), cap, chunk_records, depth,
+                                            _dptr(scratch), scratch_bytes, _stream(stream)), "srpc_gpu_pack_host")
+        return self.wire_bytes(n)
+
+    def unpack_host(self, h_wire, wire_len: int, n: int, h_cols: Sequence, chunk_records: int, scratch,
+                    scratch_bytes: int, depth: int = 3, status=None, stream=None) -> int:
+        """Unpack n records from HOST wire bytes into HOST columns (the mirror
+        of pack_host).  Returns SRPC_OK or SRPC_ERR_BOUNDS."""
+        arr = self._cols(h_cols)
+        return check(_lib.lib().srpc_gpu_unpack_host(self._h, _dptr(h_wire), wire_len, n, arr, chunk_records, depth,
+                                                     _dptr(scratch), scratch_bytes, _dptr(status), _stream(stream)),
+                     "srpc_gpu_unpack_host")
+
     # -- records as structs (AoS) ---------------------------------------------
     def _offsets(self, field_offsets: Sequence[int]) -> C.Array:
         if len(field_offsets) != len(self.schema.kinds):

@@ -1,0 +1,143 @@
+"""Host-terminated batches (ABI 7: srpc_gpu_pack_host / srpc_gpu_unpack_host):
+columns and wire bytes in pinned host memory, pipelined through a ring of
+device chunk buffers.  Every case against the oracle's wire and the host
+columns it came from; chunk sizes from 1 record to more than the batch,
+rings of 1-3 slots, the direct mode (chunk 0: the kernels on the mapped
+pinned buffers, no copies), the DWORD and TILE kernel families, an envelope prefix,
+and the unpack's statuses (a bad prefix deep in a later chunk, a short wire)
+reported batch-relative as srpc_gpu_unpack reports them."""
+import numpy as np
+import pytest
+
+import oracle
+import srpc_amd
+from srpc_amd import (QUAD, GpuPacker, Schema, SRPC_ERR_BOUNDS, SRPC_STATUS_BOUNDS, SRPC_STATUS_PREFIX)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip("no GPU", allow_module_level=True)
+
+from tests.test_gpu_parity import read_status, status_buf  # noqa: E402
+
+ALL = [oracle.BOOL, oracle.INT8, oracle.CHAR, oracle.INT16, oracle.INT32, oracle.INT64]
+NP = {oracle.BOOL: np.uint8, oracle.INT8: np.int8, oracle.CHAR: np.uint8, oracle.INT16: np.int16,
+      oracle.INT32: np.int32, oracle.INT64: np.int64}
+
+
+def host_cols(kinds, n, rng):
+    cols = []
+    for k in kinds:
+        a = rng.integers(0, 256, n * oracle.KIND_SIZE[k], dtype=np.uint8).view(NP[k]).copy()
+        if k == oracle.BOOL:
+            a &= 1
+        cols.append(a)
+    return cols
+
+
+def pinned(a: np.ndarray):
+    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8).pin_memory()
+    if a.nbytes:
+        t[:a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1).copy()))
+    return t
+
+
+def scratch_for(p, chunk, depth):
+    sb = p.host_scratch_bytes(chunk, depth)
+    t = torch.empty(sb + 256, dtype=torch.uint8, device="cuda:0")
+    return t, t.data_ptr() + (-t.data_ptr()) % 256, sb
+
+
+def plan(kind):
+    if kind == "quad":
+        return QUAD.kinds, GpuPacker(QUAD)
+    sch = Schema("S", tuple((f"f{i}", k) for i, k in enumerate(ALL)))
+    return ALL, GpuPacker.for_request(sch, "Svc_servicer::m")
+
+
+@pytest.mark.parametrize("kind", ["quad", "all_request"])
+@pytest.mark.parametrize("n,chunk,depth", [(1, 1, 1), (1000, 1, 3), (1000, 16, 2), (100_003, 4096, 3),
+                                           (100_003, 65_536, 1), (100_003, 200_000, 3), (262_144, 32_768, 3),
+                                           # chunk 0: direct, the kernels on the mapped host buffers
+                                           (1, 0, 1), (100_003, 0, 1), (262_144, 0, 3)])
+def test_host_round_trip_vs_oracle(kind, n, chunk, depth):
+    kinds, p = plan(kind)
+    rng = np.random.default_rng(n + chunk + depth)
+    cols = host_cols(kinds, n, rng)
+    want = bytes(oracle.pack(kinds, cols, n, p.prefix))
+    h_cols = [pinned(c) for c in cols]
+    h_wire = torch.full((len(want) + 16,), 0xA5, dtype=torch.uint8).pin_memory()
+    keep, sp, sb = scratch_for(p, chunk, depth)
+    if chunk == 0:
+        assert sb == 0
+    s = torch.cuda.current_stream()
+    p.pack_host(h_cols, n, h_wire, chunk, sp, sb, depth=depth, stream=s)
+    torch.cuda.synchronize()
+    assert h_wire[:len(want)].numpy().tobytes() == want
+    assert (h_wire[len(want):].numpy() == 0xA5).all()  # nothing past the batch
+    back = [pinned(np.full(c.nbytes, 0x5A, np.uint8)) for c in cols]
+    st = status_buf()
+    assert p.unpack_host(h_wire, len(want), n, back, chunk, sp, sb, depth=depth, status=st, stream=s) == 0
+    torch.cuda.synchronize()
+    assert read_status(st) == (0, 2**64 - 1)
+    for b, c in zip(back, cols):
+        assert b[:c.nbytes].numpy().tobytes() == c.tobytes()
+
+
+@pytest.mark.parametrize("n,chunk,depth", [(1000, 1, 3), (100_003, 4096, 2), (262_144, 32_768, 3)])
+def test_host_round_trip_two_streams(monkeypatch, n, chunk, depth):
+    """The pipeline with the kernels on the H2D stream (SRPC_HOST_STREAMS=2)."""
+    monkeypatch.setenv("SRPC_HOST_STREAMS", "2")
+    test_host_round_trip_vs_oracle("all_request", n, chunk, depth)
+    test_host_round_trip_vs_oracle("quad", n, chunk, depth)
+
+
+def test_host_unpack_reports_batch_relative_statuses():
+    kinds, p = plan("all_request")
+    n, chunk = 50_000, 4096
+    cols = host_cols(kinds, n, np.random.default_rng(5))
+    wire = bytearray(oracle.pack(kinds, cols, n, p.prefix))
+    rb = p.record_bytes
+    for bad in (30_001, 41_000):  # two bad prefixes in later chunks: the first is reported
+        wire[bad * rb + 3] ^= 0x40
+    h_wire = pinned(np.frombuffer(bytes(wire), np.uint8))
+    back = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
+    keep, sp, sb = scratch_for(p, chunk, 3)
+    st = status_buf()
+    p.unpack_host(h_wire, len(wire), n, back, chunk, sp, sb, status=st)
+    torch.cuda.synchronize()
+    assert read_status(st) == (SRPC_STATUS_PREFIX, 30_001)
+    # a wire short of the batch: the records that fit, BOUNDS at the first that does not
+    short = (n - 777) * rb + 5
+    back2 = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
+    st2 = status_buf()
+    assert p.unpack_host(pinned(np.frombuffer(bytes(oracle.pack(kinds, cols, n, p.prefix)), np.uint8)), short, n,
+                         back2, chunk, sp, sb, status=st2) == SRPC_ERR_BOUNDS
+    torch.cuda.synchronize()
+    assert read_status(st2) == (SRPC_STATUS_BOUNDS, n - 777)
+    for b, c in zip(back2, cols):
+        k = (n - 777) * c.itemsize
+        assert b[:k].numpy().tobytes() == c.tobytes()[:k]
+
+
+def test_host_argument_errors():
+    kinds, p = plan("quad")
+    keep, sp, sb = scratch_for(p, 1024, 2)
+    cols = [pinned(np.zeros(4096, np.uint8)) for _ in kinds]
+    h_wire = pinned(np.zeros(16 * 1024, np.uint8))
+    with pytest.raises(srpc_amd.SrpcError):  # scratch too small for the ring
+        p.pack_host(cols, 1024, h_wire, 1024, sp, sb - 256, depth=2)
+    with pytest.raises(srpc_amd.SrpcError):  # scratch not 256-byte aligned
+        p.pack_host(cols, 1024, h_wire, 1024, sp + 16, sb, depth=2)
+    with pytest.raises(srpc_amd.SrpcError):  # wire capacity short of the batch
+        p.pack_host(cols, 1024, h_wire, 1024, sp, sb, depth=2, wire_cap=16 * 1023)
+    with pytest.raises(srpc_amd.SrpcError):  # direct mode on pageable host memory (not device-mapped)
+        import numpy as _np
+        pageable = [_np.zeros(1024, _np.int32) for _ in kinds]
+        p.pack_host([a.ctypes.data for a in pageable], 1024, h_wire, 0, 0, 0, depth=1)
+    with pytest.raises(srpc_amd.SrpcError):  # ring of 0 slots
+        p.host_scratch_bytes(1024, 0)
+    strs = GpuPacker(Schema("T", (("s", oracle.STRING),)))
+    with pytest.raises(srpc_amd.SrpcError):  # string schemas have no fixed chunk
+        strs.host_scratch_bytes(1024, 2)
