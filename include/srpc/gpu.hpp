@@ -222,6 +222,29 @@ public:
         return srpc_gpu_unpack(_plan, d_wire, wire_len, n, d_cols, d_status, stream);
     }
 
+    /// Host-terminated batches (ABI 7): host columns <-> host wire bytes.
+    /// chunk_records = 0 runs the kernels on the host buffers in place (they
+    /// must be page-locked and device-mapped, e.g. hipHostMalloc; no scratch);
+    /// otherwise the batch is pipelined in chunks through `depth` device
+    /// buffers in d_scratch (host_scratch_bytes).
+    uint64_t host_scratch_bytes(uint64_t chunk_records, uint32_t depth = 3) const {
+        uint64_t b = 0;
+        srpc_plan_host_scratch_bytes(_plan, chunk_records, depth, &b);
+        return b;
+    }
+    int pack_host(const void* const* h_cols, uint64_t n, uint8_t* h_wire, uint64_t wire_cap,
+                  uint64_t chunk_records = 0, uint32_t depth = 1, void* d_scratch = nullptr,
+                  uint64_t scratch_bytes = 0, void* stream = nullptr) const {
+        return srpc_gpu_pack_host(_plan, h_cols, n, h_wire, wire_cap, chunk_records, depth, d_scratch,
+                                  scratch_bytes, stream);
+    }
+    int unpack_host(const uint8_t* h_wire, uint64_t wire_len, uint64_t n, void* const* h_cols,
+                    srpc_unpack_status* d_status = nullptr, uint64_t chunk_records = 0, uint32_t depth = 1,
+                    void* d_scratch = nullptr, uint64_t scratch_bytes = 0, void* stream = nullptr) const {
+        return srpc_gpu_unpack_host(_plan, h_wire, wire_len, n, h_cols, chunk_records, depth, d_scratch,
+                                    scratch_bytes, d_status, stream);
+    }
+
     /// Fixed-size T: n records straight from / into a device copy of a T
     /// array (the raw bytes of a std::vector<T>, one hipMemcpy), no host
     /// transpose into columns.  unpack_records writes only the leaf fields.

@@ -123,6 +123,40 @@ static int run(srpc::gpu::batch_packer<T>& bp, size_t n, Fill fill, Eq eq, Emit 
                                                              static_cast<const void*>(&proto), sizeof(void*)) == 0);
         CHECK(same);
     }
+    // host-terminated (ABI 7): pinned host columns -> host wire and back,
+    // direct (kernels on the mapped buffers) and through a 2-slot ring of
+    // 7-record chunks
+    {
+        std::vector<void*> hcols(hc.col.size()), hback(hc.col.size());
+        for (size_t f = 0; f < hc.col.size(); ++f) {
+            HIPCHECK(hipHostMalloc(&hcols[f], hc.col[f].size() + 16, hipHostMallocDefault));
+            HIPCHECK(hipHostMalloc(&hback[f], hc.col[f].size() + 16, hipHostMallocDefault));
+            std::memcpy(hcols[f], hc.col[f].data(), hc.col[f].size());
+        }
+        uint8_t* hw = nullptr;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&hw), want.size() + 16, hipHostMallocDefault));
+        const uint64_t sb = bp.host_scratch_bytes(7, 2);
+        void* scratch = nullptr;
+        HIPCHECK(hipMalloc(&scratch, sb));
+        for (uint64_t chunk : {uint64_t{0}, uint64_t{7}}) {
+            std::memset(hw, 0, want.size());
+            CHECK(bp.pack_host(hcols.data(), n, hw, want.size(), chunk, 2, scratch, sb) == SRPC_OK);
+            HIPCHECK(hipDeviceSynchronize());
+            CHECK(std::memcmp(hw, want.data(), want.size()) == 0);
+            for (size_t f = 0; f < hc.col.size(); ++f) std::memset(hback[f], 0, hc.col[f].size());
+            CHECK(bp.unpack_host(hw, want.size(), n, hback.data(), st, chunk, 2, scratch, sb) == SRPC_OK);
+            HIPCHECK(hipDeviceSynchronize());
+            HIPCHECK(hipMemcpy(&hs, st, sizeof(hs), hipMemcpyDeviceToHost));
+            CHECK(hs.flags == 0);
+            bool eqc = true;
+            for (size_t f = 0; f < hc.col.size(); ++f)
+                eqc = eqc && std::memcmp(hback[f], hc.col[f].data(), hc.col[f].size()) == 0;
+            CHECK(eqc);
+        }
+        (void)hipFree(scratch);
+        (void)hipHostFree(hw);
+        for (size_t f = 0; f < hc.col.size(); ++f) { (void)hipHostFree(hcols[f]); (void)hipHostFree(hback[f]); }
+    }
     (void)hipFree(drecs);
     for (size_t f = 0; f < hc.col.size(); ++f) { (void)hipFree(dcols[f]); (void)hipFree(dback[f]); }
     (void)hipFree(dw);
