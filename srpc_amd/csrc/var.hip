@@ -1895,6 +1895,14 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
     // the lane's record bounds stay in registers (coalesced loads, issued
     // with the prefix bytes and before the table's wait)
     const uint64_t start = i < nr ? rec_offs[r0 + i] : 0, end = i < nr ? rec_offs[r0 + i + 1] : 0;
+    // the caller's tile table: this tile's bases, loaded with the index (its
+    // round trip overlaps the index's and the stage's instead of following
+    // the scan)
+    uint64_t tab_lo = 0, tab_hi = 0;
+    if (!kOpt && table && i < ns) {
+        tab_lo = table[t * ns + i];
+        tab_hi = table[(t + 1) * ns + i];
+    }
     // the prefix's first kBlock bytes are loaded here and written to LDS after
     // the table, so their round trip overlaps the index loads (one barrier
     // less before the stage can be requested)
@@ -1976,7 +1984,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_rt(VarArgs a, RtuArgs L, 
         if (i == 0) s_inexact = 0;
         __syncthreads();
         if (i < ns) {
-            const uint64_t lo = table[t * ns + i], hi = table[(t + 1) * ns + i];
+            const uint64_t lo = tab_lo, hi = tab_hi;
             const bool ok = (t > 0 || lo == 0) && hi >= lo && hi - lo == s_tot[i] && hi <= wire_len;
             s_pre[i] = lo;
             if (!ok) s_inexact = 1;

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="two_str")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tiled", action="store_true", help="time srpc_gpu_unpack_var_tiled (the tile table) instead")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -66,15 +67,27 @@ def main():
     for _ in range(2):
         p.unpack_var(w, W, n, drec, outs, soffs, scratch, sb, None)
     torch.cuda.synchronize()
+    if args.tiled:
+        table = empty(8 * p.var_tile_table_words(n) + 16)
+        p.var_tile_table(soffs, n, table)
+        torch.cuda.synchronize()
+
+        def call():
+            p.unpack_var_tiled(w, W, n, drec, table, outs, soffs, scratch, sb, None)
+    else:
+        def call():
+            p.unpack_var(w, W, n, drec, outs, soffs, scratch, sb, None)
+    call()
+    torch.cuda.synchronize()
     fn(h, 1)
     for _ in range(args.reps):
-        p.unpack_var(w, W, n, drec, outs, soffs, scratch, sb, None)
+        call()
     torch.cuda.synchronize()
     fn(h, 1)
     wgs = h[6] or 1
     names = ["table", "dma", "parse", "scan+base", "build", "store"]
     tot = sum(h[i] for i in range(6))
-    print(f"{args.case}: {wgs} workgroups over {args.reps} calls, cycles per workgroup:")
+    print(f"{args.case}{' tiled' if args.tiled else ''}: {wgs} workgroups over {args.reps} calls, cycles per workgroup:")
     for i, nm in enumerate(names):
         print(f"  {nm:10s} {h[i] / wgs:10.0f}  ({100 * h[i] / max(tot, 1):5.1f} %)")
     print(f"  {'total':10s} {tot / wgs:10.0f}")
