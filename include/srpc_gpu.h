@@ -435,7 +435,13 @@ int srpc_gpu_fill_splitmix_i32(int32_t* const* d_cols, uint32_t nfields, uint64_
  * kernels / D2H), ordered after the work on `stream` and before what is
  * enqueued on it later.  The results equal srpc_gpu_pack / srpc_gpu_unpack
  * on the whole batch, statuses included (first_bad_record is batch-relative).
- * String schemas: SRPC_E_UNSUPPORTED. */
+ * chunk_records == 0 is the direct mode: when every host buffer is page-
+ * locked and device-mapped (hipHostMalloc, hipHostRegister, torch pin_memory)
+ * the kernels read and write them in place over PCIe, both directions at
+ * once, no scratch, no copies (else SRPC_E_INVALID, nothing launched).  The
+ * chunked mode creates its calling thread's three streams and events on
+ * first use (kept for the process); unlike the other calls it is not meant
+ * for hipGraph capture.  String schemas: SRPC_E_UNSUPPORTED. */
 int srpc_plan_host_scratch_bytes(const srpc_plan* plan, uint64_t chunk_records, uint32_t depth,
                                  uint64_t* out);
 int srpc_gpu_pack_host(const srpc_plan* plan, const void* const* h_cols, uint64_t n, uint8_t* h_wire,
