@@ -366,7 +366,10 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
 // the wave streams its wire tile through LDS in coalesced 16-byte pieces (an
 // odd dword stride per lane: no bank conflicts).  Unpack is the mirror; bytes
 // of a struct no field covers come from the fill record (fresh objects) or
-// from the struct itself (in place: the lane reads it first).
+// from the struct itself (in place: the lane reads it first).  That mirror's
+// strided whole-struct stores ran 0.78 on some boxes and 0.41 on others, so
+// the default unpack is k_unpack_aos_piece below (a lane per 16-byte piece of
+// the array: whole-line stores, 0.69 on a 0.41 box).
 struct AosLayAllKindsV {  // {vtable*, bool, int8, char, int16, int32, int64}: 32 bytes
     static constexpr int RS = 32, NF = 6;
     static constexpr int ROFF[NF] = {8, 9, 10, 12, 16, 24}, SZ[NF] = {1, 1, 1, 2, 4, 8};
