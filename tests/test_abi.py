@@ -44,6 +44,11 @@ def test_library_loads_and_answers_host_calls():
     assert L.srpc_plan_create(None, 0, None) == _lib.SRPC_E_INVALID
     assert L.srpc_plan_destroy(None) == _lib.SRPC_E_INVALID
     assert L.srpc_gpu_pack(None, None, 0, None, 0, None) == _lib.SRPC_E_INVALID
+    # ABI 7 host-terminated calls: a null plan is refused before any device work
+    out = C.c_uint64()
+    assert L.srpc_plan_host_scratch_bytes(None, 1024, 3, C.byref(out)) == _lib.SRPC_E_INVALID
+    assert L.srpc_gpu_pack_host(None, None, 1, None, 0, 0, 1, None, 0, None) == _lib.SRPC_E_INVALID
+    assert L.srpc_gpu_unpack_host(None, None, 0, 1, None, 0, 1, None, 0, None, None) == _lib.SRPC_E_INVALID
     # the timing hook only arms thread-local state; an invalid call consumes it
     assert L.srpc_time_next_call(None, None) == _lib.SRPC_OK
     assert L.srpc_time_next_call(C.c_void_p(1), None) == _lib.SRPC_OK
