@@ -233,13 +233,13 @@ public:
         return b;
     }
     int pack_host(const void* const* h_cols, uint64_t n, uint8_t* h_wire, uint64_t wire_cap,
-                  uint64_t chunk_records = 0, uint32_t depth = 1, void* d_scratch = nullptr,
+                  uint64_t chunk_records = 0, uint32_t depth = 3, void* d_scratch = nullptr,
                   uint64_t scratch_bytes = 0, void* stream = nullptr) const {
         return srpc_gpu_pack_host(_plan, h_cols, n, h_wire, wire_cap, chunk_records, depth, d_scratch,
                                   scratch_bytes, stream);
     }
     int unpack_host(const uint8_t* h_wire, uint64_t wire_len, uint64_t n, void* const* h_cols,
-                    srpc_unpack_status* d_status = nullptr, uint64_t chunk_records = 0, uint32_t depth = 1,
+                    srpc_unpack_status* d_status = nullptr, uint64_t chunk_records = 0, uint32_t depth = 3,
                     void* d_scratch = nullptr, uint64_t scratch_bytes = 0, void* stream = nullptr) const {
         return srpc_gpu_unpack_host(_plan, h_wire, wire_len, n, h_cols, chunk_records, depth, d_scratch,
                                     scratch_bytes, d_status, stream);

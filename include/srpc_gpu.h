@@ -438,10 +438,14 @@ int srpc_gpu_fill_splitmix_i32(int32_t* const* d_cols, uint32_t nfields, uint64_
  * chunk_records == 0 is the direct mode: when every host buffer is page-
  * locked and device-mapped (hipHostMalloc, hipHostRegister, torch pin_memory)
  * the kernels read and write them in place over PCIe, both directions at
- * once, no scratch, no copies (else SRPC_E_INVALID, nothing launched).  The
- * chunked mode creates its calling thread's three streams and events on
- * first use (kept for the process); unlike the other calls it is not meant
- * for hipGraph capture.  String schemas: SRPC_E_UNSUPPORTED. */
+ * once, no scratch, no copies; each buffer's pinned allocation must cover its
+ * n records (else SRPC_E_INVALID, nothing launched).  Every argument is
+ * checked before anything is enqueued.  The chunked mode borrows three
+ * streams and their events from a per-device pool (created on first use, kept
+ * for the process, grown only by calls in flight at once); unlike the other
+ * calls it is not meant for hipGraph capture.  An error part way through the
+ * chunked ring still orders everything the call enqueued before `stream`'s
+ * later work.  String schemas: SRPC_E_UNSUPPORTED. */
 int srpc_plan_host_scratch_bytes(const srpc_plan* plan, uint64_t chunk_records, uint32_t depth,
                                  uint64_t* out);
 int srpc_gpu_pack_host(const srpc_plan* plan, const void* const* h_cols, uint64_t n, uint8_t* h_wire,

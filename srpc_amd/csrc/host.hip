@@ -13,15 +13,17 @@
 // Stream semantics: the call is ordered after the work already on `stream`
 // and everything it does is ordered before the work enqueued on `stream`
 // after it (the internal streams wait on an event of `stream` first; `stream`
-// waits on the last D2H).  The internal streams and events are per host
-// thread and device, created once.  Host buffers should be pinned (pageable
-// ones work, without overlap).
+// waits on the last D2H; after an error part way through, on everything the
+// call enqueued).  The internal streams and events come from a per-device pool
+// (a call borrows a pipe and returns it), created on first use.  Host buffers
+// should be pinned (pageable ones work, without overlap).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "plan.h"
@@ -37,28 +39,105 @@ uint64_t r256(uint64_t x) { return (x + kAlignScratch - 1) & ~(kAlignScratch - 1
 struct Pipe {
     hipStream_t in = nullptr, k = nullptr, out = nullptr;
     hipEvent_t start = nullptr;
+    hipEvent_t fence[3] = {};    // an error's drain: the last work of each internal stream
     std::vector<hipEvent_t> ev;  // 3 per ring slot: input copied, kernel done, output copied
-    bool ok = false;
 };
 
-// The calling thread's streams and events on `device` (ring of `depth`).
-Pipe* pipe_for(int device, uint32_t depth) {
-    thread_local std::map<int, Pipe> pipes;
-    Pipe& p = pipes[device];
-    if (!p.ok) {
-        const unsigned fl = hipStreamNonBlocking;
-        if (hipStreamCreateWithFlags(&p.in, fl) != hipSuccess || hipStreamCreateWithFlags(&p.k, fl) != hipSuccess ||
-            hipStreamCreateWithFlags(&p.out, fl) != hipSuccess ||
-            hipEventCreateWithFlags(&p.start, hipEventDisableTiming) != hipSuccess)
-            return nullptr;
-        p.ok = true;
+// Pipes are pooled per device: a call borrows one -- any
+// free pipe, or a new one when every pipe is lent to a call in another thread
+// -- and returns it when its work is enqueued.  The pool grows to the number
+// of calls ever in flight at once, not with the threads that made them, and a
+// thread that exits leaks nothing.  Pipes live for the process (destroying
+// streams while HIP tears down at exit is not safe).  Calls from one thread on
+// different caller streams share a pipe, so their copies queue in call order
+// on its streams -- the same order the calls were made in.
+struct PipePool {
+    std::mutex mu;
+    std::map<int, std::vector<Pipe*>> free;
+    std::map<int, uint64_t> made;
+};
+PipePool& pool() {
+    static PipePool* P = new PipePool;  // never destroyed (see above)
+    return *P;
+}
+
+Pipe* make_pipe() {
+    auto* p = new Pipe;
+    const unsigned fl = hipStreamNonBlocking;
+    bool ok = hipStreamCreateWithFlags(&p->in, fl) == hipSuccess && hipStreamCreateWithFlags(&p->k, fl) == hipSuccess &&
+              hipStreamCreateWithFlags(&p->out, fl) == hipSuccess &&
+              hipEventCreateWithFlags(&p->start, hipEventDisableTiming) == hipSuccess;
+    for (auto& e : p->fence) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (ok) return p;
+    for (hipStream_t q : {p->in, p->k, p->out})
+        if (q) (void)hipStreamDestroy(q);
+    for (hipEvent_t e : {p->start, p->fence[0], p->fence[1], p->fence[2]})
+        if (e) (void)hipEventDestroy(e);
+    delete p;
+    (void)hipGetLastError();
+    return nullptr;
+}
+
+// A pipe of `device` (the current device) with a ring of `depth`, returned by
+// ~Lease.
+struct Lease {
+    int device;
+    Pipe* p = nullptr;
+    Lease(int dev, uint32_t depth) : device(dev) {
+        {
+            std::lock_guard<std::mutex> lk(pool().mu);
+            auto& v = pool().free[dev];
+            if (!v.empty()) {
+                p = v.back();
+                v.pop_back();
+            }
+        }
+        if (!p) {
+            p = make_pipe();
+            if (!p) return;
+            std::lock_guard<std::mutex> lk(pool().mu);
+            ++pool().made[dev];
+        }
+        while (p->ev.size() < 3ull * depth) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                release();
+                return;
+            }
+            p->ev.push_back(e);
+        }
     }
-    while (p.ev.size() < 3ull * depth) {
-        hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-        p.ev.push_back(e);
+    void release() {
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(pool().mu);
+        pool().free[device].push_back(p);
+        p = nullptr;
     }
-    return &p;
+    ~Lease() { release(); }
+};
+
+// The chunked ring records events on `stream` and makes the pool's streams
+// wait on them: inside a stream capture that would pull the pool's streams
+// into the caller's graph (and a later call's copies with them), so the
+// chunked mode refuses a capturing stream instead (SRPC_E_UNSUPPORTED).
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return cs != hipStreamCaptureStatusNone;
+}
+
+// After an error part way through a ring: `stream` waits on everything already
+// enqueued on the internal streams, so a caller that sees the error and then
+// reuses its host buffers or scratch (in stream order) cannot race copies that
+// are still in flight into them.  Returns rc.
+int drain(Pipe* P, hipStream_t s, int rc) {
+    hipStream_t q[3] = {P->in, P->k, P->out};
+    for (int i = 0; i < 3; ++i)
+        if (hipEventRecord(P->fence[i], q[i]) == hipSuccess) (void)hipStreamWaitEvent(s, P->fence[i], 0);
+    return rc;
 }
 
 // A chunk's status folded into the call's: flags OR'ed, its first failing
@@ -110,6 +189,14 @@ bool two_streams() {
     return e && e[0] == '2';
 }
 
+// Test hook (SRPC_HOST_FAIL_AT=k, read per call): the chunked ring fails at
+// chunk k as a HIP error would, after chunks 0..k-1 are enqueued -- the
+// error path's drain is tested with copies really in flight.
+uint64_t fail_at() {
+    const char* e = std::getenv("SRPC_HOST_FAIL_AT");
+    return e && *e ? std::strtoull(e, nullptr, 10) : UINT64_MAX;
+}
+
 int check_pipe_args(const srpc_plan* p, uint64_t chunk, uint32_t depth) {
     if (!p) return SRPC_E_INVALID;
     if (p->has_string) return SRPC_E_UNSUPPORTED;  // string batches have no fixed chunk size
@@ -118,12 +205,15 @@ int check_pipe_args(const srpc_plan* p, uint64_t chunk, uint32_t depth) {
     return SRPC_OK;
 }
 
-// Direct mode (chunk_records == 0): the device addresses of page-locked,
-// device-mapped host buffers (hipHostMalloc / hipHostRegister -- what
-// torch's pin_memory allocates), or false when any buffer is not one: the
+// Direct mode (chunk_records == 0): the device address of a page-locked,
+// device-mapped host buffer (hipHostMalloc / hipHostRegister -- what torch's
+// pin_memory allocates) whose allocation covers [h, h + bytes), or false: the
 // kernels then read and write the host memory in place over PCIe, both
-// directions at once, with no copies and no chunks.
-bool mapped(const void* h, void** d) {
+// directions at once, with no copies and no chunks.  The allocation's range
+// is the runtime's own record of the pinned block (hipMemGetAddressRange), so
+// a buffer shorter than the batch is refused instead of being read or written
+// past its end.
+bool mapped(const void* h, uint64_t bytes, void** d) {
     if (!h) return false;
     hipPointerAttribute_t at{};
     if (hipPointerGetAttributes(&at, h) != hipSuccess) {
@@ -135,7 +225,25 @@ bool mapped(const void* h, void** d) {
         (void)hipGetLastError();
         return false;
     }
-    return true;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    uintptr_t lo = reinterpret_cast<uintptr_t>(*d);  // the range in the address space it was found in
+    if (hipMemGetAddressRange(&base, &size, *d) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        if (hipMemGetAddressRange(&base, &size, const_cast<void*>(h)) != hipSuccess || !base) {
+            (void)hipGetLastError();
+            return false;
+        }
+        lo = reinterpret_cast<uintptr_t>(h);
+    }
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    return lo >= b && lo - b <= size && bytes <= size - (lo - b);
+}
+
+__global__ void k_or_bounds(srpc_unpack_status* st, uint64_t at) {
+    if (threadIdx.x) return;
+    atomicOr(&st->flags, SRPC_STATUS_BOUNDS);
+    atomicMin(reinterpret_cast<unsigned long long*>(&st->first_bad_record), static_cast<unsigned long long>(at));
 }
 
 }  // namespace
@@ -152,6 +260,8 @@ int srpc_plan_host_scratch_bytes(const srpc_plan* p, uint64_t chunk_records, uin
     return SRPC_OK;
 }
 
+// Every argument is checked before anything is enqueued; an error part way
+// through the ring drains what was enqueued into `stream` (drain()).
 int srpc_gpu_pack_host(const srpc_plan* p, const void* const* h_cols, uint64_t n, uint8_t* h_wire,
                        uint64_t wire_cap, uint64_t chunk_records, uint32_t depth, void* d_scratch,
                        uint64_t scratch_bytes, void* stream) {
@@ -161,33 +271,35 @@ int srpc_gpu_pack_host(const srpc_plan* p, const void* const* h_cols, uint64_t n
     for (uint32_t f = 0; f < p->nfields; ++f)
         if (!h_cols[f]) return SRPC_E_INVALID;
     if (n > UINT64_MAX / p->stride || n * p->stride > wire_cap) return SRPC_E_CAPACITY;
+    DeviceGuard g(p->device);
     if (chunk_records == 0) {
-        DeviceGuard g(p->device);
         const void* dc[kMaxFields];
         void* dw = nullptr;
         for (uint32_t f = 0; f < p->nfields; ++f) {
             void* d = nullptr;
-            if (!mapped(h_cols[f], &d)) return SRPC_E_INVALID;
+            if (!mapped(h_cols[f], n * p->size[f], &d)) return SRPC_E_INVALID;
             dc[f] = d;
         }
-        if (!mapped(h_wire, &dw)) return SRPC_E_INVALID;
-        return srpc_gpu_pack(p, dc, n, static_cast<uint8_t*>(dw), wire_cap, stream);
+        if (!mapped(h_wire, n * p->stride, &dw)) return SRPC_E_INVALID;
+        return srpc_gpu_pack(p, dc, n, static_cast<uint8_t*>(dw), n * p->stride, stream);
     }
     if (!d_scratch) return SRPC_E_INVALID;
     const SlotLayout L = slot_layout(p, chunk_records);
     if (scratch_bytes < depth * L.bytes) return SRPC_E_CAPACITY;
     if (reinterpret_cast<uintptr_t>(d_scratch) % kAlignScratch) return SRPC_E_ALIGN;
-    DeviceGuard g(p->device);
-    Pipe* P = pipe_for(p->device, depth);
+    auto s = static_cast<hipStream_t>(stream);
+    if (capturing(s)) return SRPC_E_UNSUPPORTED;
+    Lease lease(p->device, depth);
+    Pipe* P = lease.p;
     if (!P) return SRPC_E_HIP;
     const bool two = two_streams();
     hipStream_t ks = two ? P->in : P->k;
-    auto s = static_cast<hipStream_t>(stream);
     auto* base = static_cast<uint8_t*>(d_scratch);
     if (hipEventRecord(P->start, s) != hipSuccess) return SRPC_E_HIP;
     for (hipStream_t q : {P->in, P->k, P->out}) (void)hipStreamWaitEvent(q, P->start, 0);
-    const uint64_t nch = (n + chunk_records - 1) / chunk_records;
+    const uint64_t nch = (n + chunk_records - 1) / chunk_records, fail = fail_at();
     for (uint64_t i = 0; i < nch; ++i) {
+        if (i == fail) return drain(P, s, SRPC_E_HIP);
         const uint32_t sl = static_cast<uint32_t>(i % depth);
         hipEvent_t ev_in = P->ev[3 * sl], ev_k = P->ev[3 * sl + 1], ev_out = P->ev[3 * sl + 2];
         uint8_t* slot = base + sl * L.bytes;
@@ -205,18 +317,18 @@ int srpc_gpu_pack_host(const srpc_plan* p, const void* const* h_cols, uint64_t n
             dcols[f] = slot + L.col[f];
             if (hipMemcpyAsync(slot + L.col[f], static_cast<const uint8_t*>(h_cols[f]) + lo * p->size[f],
                                cnt * p->size[f], hipMemcpyHostToDevice, P->in) != hipSuccess)
-                return SRPC_E_HIP;
+                return drain(P, s, SRPC_E_HIP);
         }
         if (!two) {
             (void)hipEventRecord(ev_in, P->in);
             (void)hipStreamWaitEvent(P->k, ev_in, 0);
         }
-        if (int rc = srpc_gpu_pack(p, dcols, cnt, slot + L.wire, cnt * p->stride, ks)) return rc;
+        if (int rc = srpc_gpu_pack(p, dcols, cnt, slot + L.wire, cnt * p->stride, ks)) return drain(P, s, rc);
         (void)hipEventRecord(ev_k, ks);
         (void)hipStreamWaitEvent(P->out, ev_k, 0);
         if (hipMemcpyAsync(h_wire + lo * p->stride, slot + L.wire, cnt * p->stride, hipMemcpyDeviceToHost, P->out) !=
             hipSuccess)
-            return SRPC_E_HIP;
+            return drain(P, s, SRPC_E_HIP);
         (void)hipEventRecord(ev_out, P->out);
     }
     // the caller's stream after the last D2H (the copy stream runs them in order)
@@ -224,50 +336,71 @@ int srpc_gpu_pack_host(const srpc_plan* p, const void* const* h_cols, uint64_t n
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
 
+// A wire shorter than n records: the records that fit are decoded, SRPC_ERR_
+// BOUNDS is returned and the status says BOUNDS at record n_fit (srpc_gpu_
+// unpack's own semantics, in either mode).
 int srpc_gpu_unpack_host(const srpc_plan* p, const uint8_t* h_wire, uint64_t wire_len, uint64_t n,
                          void* const* h_cols, uint64_t chunk_records, uint32_t depth, void* d_scratch,
                          uint64_t scratch_bytes, srpc_unpack_status* d_status, void* stream) {
     if (int rc = check_pipe_args(p, chunk_records, depth)) return rc;
+    uint64_t n_fit = wire_len / p->stride;
+    const int ret = n_fit < n ? SRPC_ERR_BOUNDS : SRPC_OK;
+    n_fit = std::min(n_fit, n);
+    // arguments first: nothing is launched for a call that returns SRPC_E_*
+    if (n_fit && (!h_cols || !h_wire)) return SRPC_E_INVALID;
+    for (uint32_t f = 0; n_fit && f < p->nfields; ++f)
+        if (!h_cols[f]) return SRPC_E_INVALID;
     DeviceGuard g(p->device);
     auto s = static_cast<hipStream_t>(stream);
-    uint64_t n_fit = wire_len / p->stride;
-    int ret = SRPC_OK;
-    if (n_fit < n) {
-        ret = SRPC_ERR_BOUNDS;
-    } else {
-        n_fit = n;
+    void* dc[kMaxFields];
+    void* dw = nullptr;
+    if (n_fit && chunk_records == 0) {
+        for (uint32_t f = 0; f < p->nfields; ++f)
+            if (!mapped(h_cols[f], n_fit * p->size[f], &dc[f])) return SRPC_E_INVALID;
+        if (!mapped(h_wire, n_fit * p->stride, &dw)) return SRPC_E_INVALID;
     }
+    const SlotLayout L = slot_layout(p, chunk_records ? chunk_records : 1);
+    if (n_fit && chunk_records) {
+        if (!d_scratch) return SRPC_E_INVALID;
+        if (scratch_bytes < depth * L.bytes) return SRPC_E_CAPACITY;
+        if (reinterpret_cast<uintptr_t>(d_scratch) % kAlignScratch) return SRPC_E_ALIGN;
+        if (capturing(s)) return SRPC_E_UNSUPPORTED;
+    }
+    if (n_fit == 0) {
+        if (d_status) {
+            hipLaunchKernelGGL(k_host_status, dim3(1), dim3(64), 0, s, d_status, ret ? SRPC_STATUS_BOUNDS : 0u,
+                               ret ? 0ull : UINT64_MAX);
+            if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+        }
+        return ret;
+    }
+    if (chunk_records == 0) {
+        // the n_fit records that fit, then the short wire's BOUNDS on top
+        const int rc = srpc_gpu_unpack(p, static_cast<const uint8_t*>(dw), n_fit * p->stride, n_fit, dc, d_status,
+                                       stream);
+        if (rc != SRPC_OK) return rc;
+        if (ret && d_status) {
+            hipLaunchKernelGGL(k_or_bounds, dim3(1), dim3(64), 0, s, d_status, n_fit);
+            if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+        }
+        return ret;
+    }
+    Lease lease(p->device, depth);
+    Pipe* P = lease.p;
+    if (!P) return SRPC_E_HIP;
+    const bool two = two_streams();
+    hipStream_t ks = two ? P->in : P->k;
+    auto* base = static_cast<uint8_t*>(d_scratch);
     if (d_status) {
         hipLaunchKernelGGL(k_host_status, dim3(1), dim3(64), 0, s, d_status, ret ? SRPC_STATUS_BOUNDS : 0u,
                            ret ? n_fit : UINT64_MAX);
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
     }
-    if (n_fit == 0) return ret;
-    if (!h_cols || !h_wire) return SRPC_E_INVALID;
-    for (uint32_t f = 0; f < p->nfields; ++f)
-        if (!h_cols[f]) return SRPC_E_INVALID;
-    if (chunk_records == 0) {
-        void* dc[kMaxFields];
-        void* dw = nullptr;
-        for (uint32_t f = 0; f < p->nfields; ++f)
-            if (!mapped(h_cols[f], &dc[f])) return SRPC_E_INVALID;
-        if (!mapped(h_wire, &dw)) return SRPC_E_INVALID;
-        const int rc = srpc_gpu_unpack(p, static_cast<const uint8_t*>(dw), wire_len, n, dc, d_status, stream);
-        return rc;
-    }
-    if (!d_scratch) return SRPC_E_INVALID;
-    const SlotLayout L = slot_layout(p, chunk_records);
-    if (scratch_bytes < depth * L.bytes) return SRPC_E_CAPACITY;
-    if (reinterpret_cast<uintptr_t>(d_scratch) % kAlignScratch) return SRPC_E_ALIGN;
-    Pipe* P = pipe_for(p->device, depth);
-    if (!P) return SRPC_E_HIP;
-    const bool two = two_streams();
-    hipStream_t ks = two ? P->in : P->k;
-    auto* base = static_cast<uint8_t*>(d_scratch);
     if (hipEventRecord(P->start, s) != hipSuccess) return SRPC_E_HIP;
     for (hipStream_t q : {P->in, P->k, P->out}) (void)hipStreamWaitEvent(q, P->start, 0);
-    const uint64_t nch = (n_fit + chunk_records - 1) / chunk_records;
+    const uint64_t nch = (n_fit + chunk_records - 1) / chunk_records, fail = fail_at();
     for (uint64_t i = 0; i < nch; ++i) {
+        if (i == fail) return drain(P, s, SRPC_E_HIP);
         const uint32_t sl = static_cast<uint32_t>(i % depth);
         hipEvent_t ev_in = P->ev[3 * sl], ev_k = P->ev[3 * sl + 1], ev_out = P->ev[3 * sl + 2];
         uint8_t* slot = base + sl * L.bytes;
@@ -282,7 +415,7 @@ int srpc_gpu_unpack_host(const srpc_plan* p, const uint8_t* h_wire, uint64_t wir
         }
         if (hipMemcpyAsync(slot + L.wire, h_wire + lo * p->stride, cnt * p->stride, hipMemcpyHostToDevice, P->in) !=
             hipSuccess)
-            return SRPC_E_HIP;
+            return drain(P, s, SRPC_E_HIP);
         if (!two) {
             (void)hipEventRecord(ev_in, P->in);
             (void)hipStreamWaitEvent(P->k, ev_in, 0);
@@ -291,17 +424,17 @@ int srpc_gpu_unpack_host(const srpc_plan* p, const uint8_t* h_wire, uint64_t wir
         for (uint32_t f = 0; f < p->nfields; ++f) dcols[f] = slot + L.col[f];
         auto* cst = d_status ? reinterpret_cast<srpc_unpack_status*>(slot + L.status) : nullptr;
         const int rc = srpc_gpu_unpack(p, slot + L.wire, cnt * p->stride, cnt, dcols, cst, ks);
-        if (rc != SRPC_OK) return rc;
+        if (rc != SRPC_OK) return drain(P, s, rc);
         if (cst) {
             hipLaunchKernelGGL(k_merge_status, dim3(1), dim3(64), 0, ks, d_status, cst, lo);
-            if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
+            if (hipGetLastError() != hipSuccess) return drain(P, s, SRPC_E_HIP);
         }
         (void)hipEventRecord(ev_k, ks);
         (void)hipStreamWaitEvent(P->out, ev_k, 0);
         for (uint32_t f = 0; f < p->nfields; ++f)
             if (hipMemcpyAsync(static_cast<uint8_t*>(h_cols[f]) + lo * p->size[f], slot + L.col[f], cnt * p->size[f],
                                hipMemcpyDeviceToHost, P->out) != hipSuccess)
-                return SRPC_E_HIP;
+                return drain(P, s, SRPC_E_HIP);
         (void)hipEventRecord(ev_out, P->out);
     }
     (void)hipStreamWaitEvent(s, P->ev[3 * ((nch - 1) % depth) + 2], 0);
@@ -309,3 +442,12 @@ int srpc_gpu_unpack_host(const srpc_plan* p, const uint8_t* h_wire, uint64_t wir
 }
 
 }  // extern "C"
+
+// Test hook (not in include/): pipes the host-terminated calls have created on
+// `device` (the pool's size), to check that it grows with concurrency, not with
+// the number of threads that made calls.
+extern "C" __attribute__((visibility("default"))) uint64_t srpc_debug_host_pipes(int device) {
+    std::lock_guard<std::mutex> lk(pool().mu);
+    auto it = pool().made.find(device);
+    return it == pool().made.end() ? 0 : it->second;
+}

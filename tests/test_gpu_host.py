@@ -141,3 +141,142 @@ def test_host_argument_errors():
     strs = GpuPacker(Schema("T", (("s", oracle.STRING),)))
     with pytest.raises(srpc_amd.SrpcError):  # string schemas have no fixed chunk
         strs.host_scratch_bytes(1024, 2)
+
+
+def _hip():
+    import ctypes
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    lib.hipHostFree.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+def test_host_direct_refuses_short_pinned_allocations():
+    """Direct mode checks each pinned allocation's extent (the runtime's own
+    record of it), not only that its base is mapped: a wire or column buffer
+    shorter than the batch is refused before anything runs."""
+    import ctypes
+    hip = _hip()
+    kinds, p = plan("quad")
+    n = 65_536                     # 1 MiB of wire, 256 KiB per column: four times the 64 KiB allocation
+    small = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(small), 64 * 1024, 0) == 0
+    try:
+        cols = host_cols(kinds, n, np.random.default_rng(1))
+        h_cols = [pinned(c) for c in cols]
+        h_wire = pinned(np.zeros(16 * n, np.uint8))
+        with pytest.raises(srpc_amd.SrpcError):   # a wire allocation short of the batch
+            p.pack_host(h_cols, n, small.value, 0, 0, 0, depth=1, wire_cap=16 * n)
+        with pytest.raises(srpc_amd.SrpcError):   # one column's allocation short of the batch
+            p.pack_host(h_cols[:3] + [small.value], n, h_wire, 0, 0, 0, depth=1)
+        with pytest.raises(srpc_amd.SrpcError):   # unpack into a short column
+            p.unpack_host(h_wire, 16 * n, n, h_cols[:3] + [small.value], 0, 0, 0, depth=1)
+        # the same allocation is accepted for a batch it covers
+        p.pack_host(h_cols, 4096, small.value, 0, 0, 0, depth=1, wire_cap=16 * 4096)
+        torch.cuda.synchronize()
+        want = bytes(oracle.pack(kinds, [c[:4096] for c in cols], 4096))
+        assert ctypes.string_at(small.value, len(want)) == want
+    finally:
+        torch.cuda.synchronize()
+        hip.hipHostFree(small)
+
+
+def test_host_direct_short_wire_reports_bounds():
+    """Direct mode, a wire shorter than the batch: the records that fit, then
+    (SRPC_ERR_BOUNDS, first bad = the first record that does not fit)."""
+    kinds, p = plan("all_request")
+    n = 30_000
+    cols = host_cols(kinds, n, np.random.default_rng(9))
+    wire = bytes(oracle.pack(kinds, cols, n, p.prefix))
+    rb = p.record_bytes
+    short = (n - 321) * rb + 7
+    back = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
+    st = status_buf()
+    assert p.unpack_host(pinned(np.frombuffer(wire, np.uint8)), short, n, back, 0, 0, 0, depth=1,
+                         status=st) == SRPC_ERR_BOUNDS
+    torch.cuda.synchronize()
+    assert read_status(st) == (SRPC_STATUS_BOUNDS, n - 321)
+    for b, c in zip(back, cols):
+        k = (n - 321) * c.itemsize
+        assert b[:k].numpy().tobytes() == c.tobytes()[:k]
+    # no record fits: BOUNDS at 0, nothing decoded
+    st0 = status_buf()
+    assert p.unpack_host(pinned(np.frombuffer(wire, np.uint8)), rb - 1, n, back, 0, 0, 0, depth=1,
+                         status=st0) == SRPC_ERR_BOUNDS
+    torch.cuda.synchronize()
+    assert read_status(st0) == (SRPC_STATUS_BOUNDS, 0)
+
+
+def test_host_pipe_pool_grows_with_concurrency_not_threads():
+    """the chunked calls borrow their streams from a per-device
+    pool.  64 short-lived threads, one after another, add at most one pipe;
+    4 threads at once add at most 4."""
+    import ctypes
+    import threading
+    hook = srpc_amd._lib.lib().srpc_debug_host_pipes
+    hook.argtypes, hook.restype = [ctypes.c_int], ctypes.c_uint64
+    kinds, p = plan("quad")
+    n, chunk = 20_000, 4096
+    cols = host_cols(kinds, n, np.random.default_rng(2))
+    want = bytes(oracle.pack(kinds, cols, n))
+    h_cols = [pinned(c) for c in cols]
+    keep = [scratch_for(p, chunk, 3) for _ in range(4)]
+    wires = [pinned(np.zeros(len(want), np.uint8)) for _ in range(4)]
+    errs = []
+
+    def one(i):
+        try:
+            _, sp, sb = keep[i]
+            s = torch.cuda.Stream()
+            p.pack_host(h_cols, n, wires[i], chunk, sp, sb, depth=3, stream=s)
+            s.synchronize()
+            assert wires[i].numpy().tobytes() == want
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    one(0)
+    base = hook(0)
+    for _ in range(64):
+        t = threading.Thread(target=one, args=(0,))
+        t.start()
+        t.join()
+    assert not errs and hook(0) - base <= 1, (errs, hook(0) - base)
+    ts = [threading.Thread(target=one, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and hook(0) - base <= 4, (errs, hook(0) - base)
+
+
+@pytest.mark.parametrize("direction", ["pack", "unpack"])
+def test_host_ring_error_drains_into_callers_stream(monkeypatch, direction):
+    """An error part way through the chunked ring (injected at chunk 14 of 16,
+    SRPC_HOST_FAIL_AT) returns it, and the caller's stream is ordered after
+    every copy the call already enqueued: once that stream is synchronized,
+    chunks 0..13 are complete in the host buffers."""
+    kinds, p = plan("quad")
+    n, chunk = 16 * 65_536, 65_536
+    cols = host_cols(kinds, n, np.random.default_rng(3))
+    want = bytes(oracle.pack(kinds, cols, n))
+    keep, sp, sb = scratch_for(p, chunk, 3)
+    s = torch.cuda.Stream()
+    monkeypatch.setenv("SRPC_HOST_FAIL_AT", "14")
+    done = 14 * chunk
+    if direction == "pack":
+        h_cols = [pinned(c) for c in cols]
+        h_wire = pinned(np.zeros(len(want), np.uint8))
+        with pytest.raises(srpc_amd.SrpcError):
+            p.pack_host(h_cols, n, h_wire, chunk, sp, sb, depth=3, stream=s)
+        s.synchronize()
+        assert h_wire[:done * 16].numpy().tobytes() == want[:done * 16]
+    else:
+        h_wire = pinned(np.frombuffer(want, np.uint8))
+        back = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
+        with pytest.raises(srpc_amd.SrpcError):
+            p.unpack_host(h_wire, len(want), n, back, chunk, sp, sb, depth=3, stream=s)
+        s.synchronize()
+        for b, c in zip(back, cols):
+            assert b[:done * c.itemsize].numpy().tobytes() == c.tobytes()[:done * c.itemsize]
+    monkeypatch.delenv("SRPC_HOST_FAIL_AT")
+    torch.cuda.synchronize()
