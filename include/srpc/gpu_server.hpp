@@ -270,6 +270,14 @@ public:
     uint64_t buffer_bytes() const { return _max * max_fin(); }
 
     /// Serve one connected socket until the peer closes it.
+    ///
+    /// Servers whose methods are all fixed-size run two batches in flight:
+    /// batch k's copies and kernels are enqueued (process_begin) and the next
+    /// batch is received into the other half of the double-buffered pinned
+    /// staging while they run; batch k's answers are sent (process_end) once
+    /// batch k + 1 is enqueued -- or before any recv that would block, so a
+    /// peer that waits for every answer before it closes is never kept
+    /// waiting.  Answers leave in request order.
     batch_stats serve_connection(int fd) {
         if (_m.empty()) throw plan_error("batch_server::serve_connection (no methods)", SRPC_E_INVALID);
         check(hipSetDevice(_dev));
@@ -281,8 +289,20 @@ public:
         uint64_t nf = 0;
         bool eof = false;
         bool buffered = false;  // whole frames already wait in _h_in: walk them before blocking in recv
+        int cur = 0;            // the staging slot frames are received into
+        use_slot(cur);
+        pending pend;
+        auto finish = [&] {
+            if (!pend.valid) return;
+            use_slot(pend.slot);
+            process_end(fd, pend, st);
+            pend.valid = false;
+            use_slot(cur);
+        };
         while (true) {
             if (!eof && !buffered) {
+                // answer a batch in flight before a recv that would block
+                if (pend.valid && !more_pending(fd)) finish();
                 // cap - have > 0 here: a full buffer is always consumed below,
                 // so recv returning 0 is the peer's orderly shutdown
                 auto t0 = clock::now();
@@ -315,12 +335,31 @@ public:
                 continue;
             }
             if (!full && !eof && more_pending(fd)) continue;  // fill the batch while data streams in
-            if (nf) process(fd, nf, walked, st);
-            std::memmove(_h_in, _h_in + walked, have - walked);
+            if (nf) {
+                if (_nslots == 2) {
+                    pending p = process_begin(nf, walked, st);
+                    p.slot = cur;
+                    finish();  // the previous batch's answers: its work ran while this one arrived
+                    pend = p;
+                    // the rest of the buffer (a cut frame) continues in the other slot
+                    const int nxt = cur ^ 1;
+                    std::memcpy(_slots[nxt].h_in, _h_in + walked, have - walked);
+                    cur = nxt;
+                    use_slot(cur);
+                } else {
+                    pending p = process_begin(nf, walked, st);
+                    p.slot = cur;
+                    process_end(fd, p, st);
+                    std::memmove(_h_in, _h_in + walked, have - walked);
+                }
+            } else {
+                std::memmove(_h_in, _h_in + walked, have - walked);
+            }
             have -= walked;
             walked = 0;
             nf = 0;
             if (oversize) {
+                finish();
                 if (!serve_oversize(fd, have, st)) return st;
                 have = 0;
             }
@@ -330,6 +369,7 @@ public:
             // them before the next recv, which would block.
             buffered = have >= 4 && have - 4 >= be32_at(_h_in);
         }
+        finish();
         return st;  // bytes of a cut final frame are dropped, as the reference's recv_data does
     }
 
@@ -466,14 +506,25 @@ private:
             check(hipHostMalloc(reinterpret_cast<void**>(&_h_out_off), 8 * (_max + 1) + 16, hipHostMallocDefault));
         }
         const uint64_t out_cap = this->out_cap();
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_in), _cap + 16, hipHostMallocDefault));
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_offs), 4 * _max + 16, hipHostMallocDefault));
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_out), out_cap + 16, hipHostMallocDefault));
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_cls), _max + 16, hipHostMallocDefault));
+        // two staging slots (two batches in flight) unless a string method's
+        // batches need the host between their kernels (SRPC_SERVER_SLOTS=1:
+        // one batch at a time, the A/B baseline)
+        const char* slots_env = std::getenv("SRPC_SERVER_SLOTS");
+        _nslots = any_var_method() || (slots_env && slots_env[0] == '1') ? 1 : 2;
+        for (int i = 0; i < _nslots; ++i) {
+            slot& z = _slots[i];
+            check(hipHostMalloc(reinterpret_cast<void**>(&z.h_in), _cap + 16, hipHostMallocDefault));
+            check(hipHostMalloc(reinterpret_cast<void**>(&z.h_offs), 4 * _max + 16, hipHostMallocDefault));
+            check(hipHostMalloc(reinterpret_cast<void**>(&z.h_out), out_cap + 16, hipHostMallocDefault));
+            check(hipHostMalloc(reinterpret_cast<void**>(&z.h_cls), _max + 16, hipHostMallocDefault));
+            // per method: its unpack status [k], its pack status [K + k] (each
+            // call resets its own, so methods never clear each other's)
+            check(hipHostMalloc(reinterpret_cast<void**>(&z.h_status), 2 * K * sizeof(srpc_unpack_status),
+                                hipHostMallocDefault));
+            check(hipEventCreateWithFlags(&z.done, hipEventDisableTiming));
+        }
+        use_slot(0);
         check(hipHostMalloc(reinterpret_cast<void**>(&_h_counts), 8 * (K + 2) + 16, hipHostMallocDefault));
-        // per method: its unpack status [k], its pack status [K + k] (each call
-        // resets its own, so methods never clear each other's)
-        check(hipHostMalloc(reinterpret_cast<void**>(&_h_status), 2 * K * sizeof(srpc_unpack_status), hipHostMallocDefault));
         check(hipMalloc(&_d_in, _cap + 16));
         check(hipMalloc(&_d_offs, 4 * _max + 16));
         check(hipMalloc(&_d_cls, _max + 16));
@@ -645,9 +696,15 @@ private:
         for (void* p : {_d_in, _d_offs, _d_cls, _d_index, _d_counts, _d_out_off, _d_gather, _d_resp, _d_out,
                         static_cast<void*>(_d_status), _d_scratch})
             if (p) (void)hipFree(p);
-        for (void* p : {static_cast<void*>(_h_in), static_cast<void*>(_h_offs), static_cast<void*>(_h_out),
-                        static_cast<void*>(_h_cls), static_cast<void*>(_h_counts), static_cast<void*>(_h_status)})
-            if (p) (void)hipHostFree(p);
+        for (slot& z : _slots) {
+            for (void* p : {static_cast<void*>(z.h_in), static_cast<void*>(z.h_offs), static_cast<void*>(z.h_out),
+                            static_cast<void*>(z.h_cls), static_cast<void*>(z.h_status)})
+                if (p) (void)hipHostFree(p);
+            if (z.done) (void)hipEventDestroy(z.done);
+            z = slot{};
+        }
+        _nslots = 0;
+        if (_h_counts) (void)hipHostFree(_h_counts);
         _d_in = _d_offs = _d_cls = _d_index = _d_counts = _d_out_off = _d_gather = _d_resp = _d_out = _d_scratch =
             nullptr;
         _d_status = nullptr;
@@ -657,8 +714,28 @@ private:
         _h_status = nullptr;
     }
 
-    /// The GPU path for the nf whole frames in _h_in[0, used).
-    void process(int fd, uint64_t nf, uint64_t used, batch_stats& st) {
+    /// A batch between process_begin and process_end.
+    struct pending {
+        bool valid = false;
+        int slot = 0;
+        uint64_t nf = 0, used = 0, unknown = 0, total = 0;
+        bool any_var = false, mixed = false;
+        double gpu_s = 0;  // host time spent on the batch's GPU work (enqueue, syncs, the final wait)
+    };
+    void use_slot(int i) {
+        slot& z = _slots[i];
+        _h_in = z.h_in;
+        _h_offs = z.h_offs;
+        _h_out = z.h_out;
+        _h_cls = z.h_cls;
+        _h_status = z.h_status;
+    }
+
+    /// The GPU path for the nf whole frames in _h_in[0, used): every copy and
+    /// kernel enqueued (with the host syncs the batch's own decisions need:
+    /// its bucket counts, a string method's response sizes), the last copy
+    /// marked by the slot's event.  process_end answers it.
+    pending process_begin(uint64_t nf, uint64_t used, batch_stats& st) {
         auto t0 = clock::now();
         auto mark = [&](const char* what) {
             if (_trace) std::fprintf(stderr, "batch %llu nf %llu %-10s %.3f ms\n", (unsigned long long)st.gpu_batches,
@@ -792,8 +869,33 @@ private:
         check(hipMemcpyAsync(_h_status, _d_status, 2 * static_cast<uint64_t>(K) * sizeof(srpc_unpack_status),
                              hipMemcpyDeviceToHost, _s));
         mark("d2h");
-        check(hipStreamSynchronize(_s));
-        mark("sync2");
+        pending pd;
+        for (int i = 0; i < _nslots; ++i)
+            if (_slots[i].h_in == _h_in) pd.slot = i;
+        check(hipEventRecord(_slots[pd.slot].done, _s));
+        pd.valid = true;
+        pd.nf = nf;
+        pd.used = used;
+        pd.unknown = unknown;
+        pd.total = total;
+        pd.any_var = any_var;
+        pd.mixed = mixed;
+        pd.gpu_s = secs(t0);
+        return pd;
+    }
+
+    /// Wait for a batch's last copy (its slot's buffers in use), check its
+    /// statuses and send its answers: the GPU's in runs, the CPU's in their
+    /// places.
+    void process_end(int fd, pending const& pd, batch_stats& st) {
+        const int K = static_cast<int>(_m.size());
+        const uint64_t nf = pd.nf, used = pd.used, unknown = pd.unknown, total = pd.total;
+        const bool any_var = pd.any_var, mixed = pd.mixed, var_methods = !_var_idx.empty();
+        auto t0 = clock::now();
+        check(hipEventSynchronize(_slots[pd.slot].done));
+        if (_trace)
+            std::fprintf(stderr, "batch %llu nf %llu wait       %.3f ms\n", (unsigned long long)st.gpu_batches,
+                         (unsigned long long)nf, 1e3 * secs(t0));
         // classification already matched every prefix and length (and walked
         // string records to their frame's end), and string responses were
         // checked against their columns before packing: a status here means
@@ -803,7 +905,7 @@ private:
                 throw plan_error(k < K ? "batch_server: classified frame failed to unpack"
                                        : "batch_server: string responses overran a sized wire",
                                  SRPC_E_INVALID);
-        const double dt = secs(t0);
+        const double dt = pd.gpu_s + secs(t0);
         if (st.gpu_batches == 0 && st.fallback_requests == 0) st.first_batch_seconds = dt;
         st.gpu_seconds += dt;
         st.h2d_bytes += used + 4 * nf;
@@ -931,12 +1033,23 @@ private:
     std::vector<uint8_t> _flat;
     uint64_t _cap = 0, _scratch_bytes = 0;
     bool _trace = std::getenv("SRPC_SERVER_TRACE") != nullptr;  // per-recv / per-batch timeline on stderr
+    // the staging slot in use (the pinned buffers of _slots[i], use_slot)
     uint8_t* _h_in = nullptr;
     uint32_t* _h_offs = nullptr;
     uint8_t* _h_out = nullptr;
     uint8_t* _h_cls = nullptr;
     uint64_t* _h_counts = nullptr;
     srpc_unpack_status* _h_status = nullptr;
+    struct slot {
+        uint8_t* h_in = nullptr;
+        uint32_t* h_offs = nullptr;
+        uint8_t* h_out = nullptr;
+        uint8_t* h_cls = nullptr;
+        srpc_unpack_status* h_status = nullptr;
+        hipEvent_t done = nullptr;  // the batch's last copy
+    };
+    slot _slots[2];
+    int _nslots = 0;
     void *_d_in = nullptr, *_d_offs = nullptr, *_d_cls = nullptr, *_d_index = nullptr, *_d_counts = nullptr,
          *_d_out_off = nullptr, *_d_gather = nullptr, *_d_resp = nullptr, *_d_out = nullptr, *_d_scratch = nullptr;
     srpc_unpack_status* _d_status = nullptr;

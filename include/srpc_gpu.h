@@ -66,7 +66,7 @@ typedef enum srpc_kind {
 #define SRPC_E_INVALID (-1)     /* bad argument or schema                       */
 #define SRPC_E_ALIGN (-2)       /* a device pointer violates the alignment rule */
 #define SRPC_E_HIP (-3)         /* HIP runtime / launch failure                 */
-#define SRPC_E_UNSUPPORTED (-4) /* schema shape this build has no kernel for    */
+#define SRPC_E_UNSUPPORTED (-4) /* no kernel for this schema / layout; chunked host call in a capture */
 #define SRPC_E_CAPACITY (-5)    /* output buffer too small                      */
 #define SRPC_ERR_BOUNDS 2       /* wire shorter than n records; the records that
                                    fit were decoded, the status says where the

@@ -330,7 +330,9 @@ bool launch_aos_run(const AosArgs& a, bool pack, const uint8_t* src, uint8_t* ds
     // the struct fits the fill record (the run kernels' strided stores: 0.65
     // into fresh objects, profiles/r04z_aos_piece_ab.log)
     const uint64_t gpn = (n + 255) / 256;
-    const bool pieces = !pack && g_aos_run_piece && aligned(dst, 16) && a.rstride <= kAosFillMax && gpn <= 0x7fffffffull;
+    // (16-byte wire loads: the wire 16-byte aligned too, else the lane-per-struct kernels)
+    const bool pieces = !pack && g_aos_run_piece && aligned(dst, 16) && aligned(src, 16) && a.rstride <= kAosFillMax &&
+                        gpn <= 0x7fffffffull;
     const dim3 gp(static_cast<uint32_t>(gpn));
 #define SRPC_AOS_RUN(Wb)                                                                                         \
     if (a.wstride == Wb) {                                                                                       \

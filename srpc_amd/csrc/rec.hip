@@ -273,6 +273,83 @@ __global__ __launch_bounds__(kRecWave) void k_unpack_rec(RecArgs a, const uint8_
     }
 }
 
+// ---- enveloped records: pack straight into 16-byte wire chunks --------------
+// A request record is mostly its envelope (49-55 of 53-63 bytes are the same
+// in every record), so the wire is a periodic template -- 16 records = S
+// chunks of 16 bytes -- with each record's field bytes (one run of V <= 16
+// bytes after the P >= 16 prefix bytes: at most one run meets a chunk) merged
+// in.  A lane per chunk: the period's template chunk from LDS, the run's
+// record and offset from the chunk index (32-bit math on constants), its
+// field values loaded from the columns, a masked 128-bit merge, one
+// non-temporal 16-byte store.  No LDS image, no barrier after the template:
+// the generic TILE pack scatters 4-byte values into its image at odd offsets
+// (misaligned LDS stores) and is at 0.71-0.75 of peak on these layouts.
+template <class L, int U>
+__global__ __launch_bounds__(kBlock) void k_pack_env(RecArgs a, uint8_t* __restrict__ wire, uint64_t nch) {
+    constexpr int S = L::STRIDE, P = L::off(0), V = S - P;
+    static_assert(P >= 16 && V <= 16 && V % 4 == 0, "one value run of whole dwords per 16-byte chunk");
+    typedef unsigned __int128 u128;
+    __shared__ uint32_t tmpl[4 * S];  // one period: S chunks = 16 records
+    for (int t = threadIdx.x; t < 4 * S; t += kBlock) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int b = (4 * t + j) % S;
+            v |= (b < P ? static_cast<uint32_t>(a.pre[b]) : 0u) << (8 * j);
+        }
+        tmpl[t] = v;
+    }
+    __syncthreads();
+    const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * (U * kBlock) + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t c = c0 + static_cast<uint64_t>(u) * kBlock;
+        if (c >= nch) break;
+        const uint64_t T = c / S;                                  // period: records 16 T ..
+        const uint32_t tc = static_cast<uint32_t>(c - T * S);     // chunk in the period
+        const uint32_t lb = 16 * tc;                               // its first byte in the period
+        const v4u tv = reinterpret_cast<const v4u*>(tmpl)[tc];
+        u128 out = (static_cast<u128>((static_cast<uint64_t>(tv.w) << 32) | tv.z) << 64) |
+                   ((static_cast<uint64_t>(tv.y) << 32) | tv.x);
+        const int32_t e = static_cast<int32_t>(lb) + 15 - P;      // >= 0: some run starts by the chunk's end
+        if (e >= 0) {
+            const uint32_t lr = static_cast<uint32_t>(e) / S;      // that record, in the period
+            const int32_t o = static_cast<int32_t>(S * lr + P) - static_cast<int32_t>(lb);  // (-V, 16)
+            if (o + V > 0) {
+                const uint64_t r = 16 * T + lr;
+                u128 val = 0;
+                static_for<L::NF>([&](auto fc) {
+                    constexpr int f = decltype(fc)::value;
+                    constexpr int at = L::off(f) - P;
+                    static_assert(L::SZ[f] == 4 || L::SZ[f] == 8, "dword fields");
+                    if constexpr (L::SZ[f] == 4) {
+                        const uint32_t x = reinterpret_cast<const uint32_t*>(a.col[f])[r];
+                        val |= static_cast<u128>(x) << (8 * at);
+                    } else {
+                        const uint64_t x = reinterpret_cast<const uint64_t*>(a.col[f])[r];
+                        val |= static_cast<u128>(x) << (8 * at);
+                    }
+                });
+                u128 m = V == 16 ? ~static_cast<u128>(0) : ((static_cast<u128>(1) << (8 * V)) - 1);
+                if (o >= 0) {
+                    val <<= 8 * o;
+                    m <<= 8 * o;
+                } else {
+                    val >>= -8 * o;
+                    m >>= -8 * o;
+                }
+                out = (out & ~m) | (val & m);
+            }
+        }
+        const uint64_t lo = static_cast<uint64_t>(out), hi = static_cast<uint64_t>(out >> 64);
+        __builtin_nontemporal_store(v4u{static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32),
+                                        static_cast<uint32_t>(hi), static_cast<uint32_t>(hi >> 32)},
+                                    reinterpret_cast<v4u*>(wire) + c);
+    }
+}
+
+constexpr int kEnvU = 4;  // chunks per lane
+
 // ---- instances ---------------------------------------------------------------
 struct RecKernel {
     bool use_pack, use_unpack;  // measured faster than the generic kernels (rec_default)
@@ -283,13 +360,21 @@ struct RecKernel {
     size_t lds;
     void (*pack)(RecArgs, uint8_t*);
     void (*unpack)(RecArgs, const uint8_t*, srpc_unpack_status*);
+    void (*env_pack)(RecArgs, uint8_t*, uint64_t);  // enveloped layouts: the chunk pack (16-record periods)
+    int stride;
 };
 
 template <class L, int G, int K>
 constexpr RecKernel make_rec(bool use_pack, bool use_unpack) {
     RecKernel r{use_pack, use_unpack, L::off(0), L::NF, {}, kRecWave * G * K, static_cast<size_t>(kRecWave) * G * K * L::STRIDE,
-                k_pack_rec<L, G, K>, k_unpack_rec<L, G, K>};
+                k_pack_rec<L, G, K>, k_unpack_rec<L, G, K>, nullptr, L::STRIDE};
     for (int f = 0; f < L::NF; ++f) r.size[f] = L::SZ[f];
+    return r;
+}
+template <class L, int G, int K>
+constexpr RecKernel make_rec_env(bool use_pack, bool use_unpack) {
+    RecKernel r = make_rec<L, G, K>(use_pack, use_unpack);
+    r.env_pack = k_pack_env<L, kEnvU>;
     return r;
 }
 
@@ -306,10 +391,11 @@ const RecKernel kRec[] = {
     // record's tile is ~14 KiB of LDS, ~11 waves per CU instead of ~5 at K =
     // 2), the short responses at K = 2.
     make_rec<Lay<0, 1, 1, 1, 2, 4, 8>, 4, 4>(true, true),  // 0.64 / 0.68 -> 0.80 / 0.72
-    make_rec<Lay<49, 4>, 4, 1>(false, true),                // unpack 0.76 -> 0.77
+    make_rec_env<Lay<49, 4>, 4, 1>(true, true),             // unpack 0.76 -> 0.77; pack 0.715 -> 0.755 (chunk kernel)
     make_rec<Lay<15, 4>, 4, 2>(false, true),                // 0.74 -> 0.77
-    make_rec<Lay<50, 4, 4>, 4, 1>(false, true),             // 0.72 (K = 2) -> 0.76
-    make_rec<Lay<55, 4, 4>, 4, 1>(false, true),             // 0.69 -> 0.78
+    make_rec_env<Lay<50, 4, 4>, 4, 1>(true, true),          // 0.72 (K = 2) -> 0.76; pack 0.75 -> 0.765 (chunk)
+    make_rec<Lay<55, 4, 4>, 4, 1>(false, true),             // 0.69 -> 0.78; pack: the generic TILE kernel
+                                                            // (0.77-0.79; the chunk kernel 0.74, r05)
     make_rec<Lay<19, 4, 4>, 4, 2>(false, true),             // 0.76 (K = 4) -> 0.78
 };
 constexpr int kNumRec = sizeof(kRec) / sizeof(kRec[0]);
@@ -332,7 +418,10 @@ bool rec_default(int id, bool pack) {
     return id >= 0 && id < kNumRec && (pack ? kRec[id].use_pack : kRec[id].use_unpack);
 }
 
-uint64_t rec_tile_records(int id) { return id >= 0 && id < kNumRec ? static_cast<uint64_t>(kRec[id].tile_records) : 0; }
+uint64_t rec_tile_records(int id, bool pack) {
+    if (id < 0 || id >= kNumRec) return 0;
+    return pack && kRec[id].env_pack ? 16 : static_cast<uint64_t>(kRec[id].tile_records);
+}
 
 static RecArgs rec_args(const srpc_plan* p, const void* const* cols) {
     RecArgs a{};
@@ -345,6 +434,13 @@ int rec_pack(int id, const srpc_plan* p, const void* const* cols, uint64_t tiles
     if (id < 0 || id >= kNumRec || !tiles) return SRPC_OK;
     if (tiles > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
     const RecKernel& r = kRec[id];
+    if (r.env_pack) {  // tiles of 16 records = `stride` 16-byte chunks
+        const uint64_t nch = tiles * static_cast<uint64_t>(r.stride);
+        const uint64_t g = (nch + kEnvU * kBlock - 1) / (kEnvU * kBlock);
+        if (g > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(r.env_pack, dim3(static_cast<uint32_t>(g)), dim3(kBlock), 0, s, rec_args(p, cols), wire, nch);
+        return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
+    }
     launch(r.pack, dim3(static_cast<uint32_t>(tiles)), dim3(kRecWave), static_cast<uint32_t>(r.lds), s, rec_args(p, cols),
            wire);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;

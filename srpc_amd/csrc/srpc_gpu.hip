@@ -1090,7 +1090,7 @@ const char* srpc_status_string(int code) {
     case SRPC_E_INVALID: return "invalid argument or schema";
     case SRPC_E_ALIGN: return "device pointer misaligned";
     case SRPC_E_HIP: return "HIP runtime error";
-    case SRPC_E_UNSUPPORTED: return "schema not supported by this build";
+    case SRPC_E_UNSUPPORTED: return "not supported (a schema or layout this build has no kernel for, or a chunked host call in a stream capture)";
     case SRPC_E_CAPACITY: return "output buffer too small";
     case SRPC_ERR_BOUNDS: return "wire shorter than the requested records";
     default: return "unknown status";
@@ -1298,7 +1298,7 @@ int srpc_gpu_pack(const srpc_plan* p, const void* const* cols, uint64_t n, uint8
     // ones for the rest
     const void* rest[kMaxFields];
     if (p->rec_pack && check_cols_aligned(cols, p->nfields, 16)) {
-        const uint64_t TR = rec_tile_records(p->rec_id), tiles = n / TR;
+        const uint64_t TR = rec_tile_records(p->rec_id, true), tiles = n / TR;
         if (tiles) {
             if (int rc2 = rec_pack(p->rec_id, p, cols, tiles, wire, s)) return rc2;
             const uint64_t done = tiles * TR;
@@ -1375,7 +1375,7 @@ int srpc_gpu_unpack(const srpc_plan* p, const uint8_t* wire, uint64_t wire_len, 
     uint64_t base = 0;  // records before `wire` (status reports of the generic kernels)
     if (p->path == SRPC_PATH_TILE && p->rec_unpack &&
         check_cols_aligned(reinterpret_cast<const void* const*>(cols), p->nfields, 16)) {
-        const uint64_t TR = rec_tile_records(p->rec_id), tiles = n_fit / TR;
+        const uint64_t TR = rec_tile_records(p->rec_id, false), tiles = n_fit / TR;
         if (tiles) {
             if (int rc2 = rec_unpack(p->rec_id, p, wire, tiles, cols, st, s)) return rc2;
             base = tiles * TR;

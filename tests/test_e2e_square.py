@@ -15,9 +15,12 @@ from tools import build_tools
 pytestmark = pytest.mark.gpu
 
 
-def _run(*args, timeout=300):
+def _run(*args, timeout=300, slots=None):
     exe = build_tools.build("e2e_square")
-    out = subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ)
+    if slots is not None:
+        env["SRPC_SERVER_SLOTS"] = slots
+    out = subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     return json.loads(out.stdout.strip().splitlines()[-1])
 
@@ -86,6 +89,20 @@ def test_e2e_mixed_methods_some_on_the_cpu():
     t = r["traffic"]
     assert g["fallback_requests"] == t["add"] + t["subtract"] + t["multiply"] + t["divide"] + t["poison"]
     assert t["poison"] == 3
+
+
+@pytest.mark.parametrize("slots", ["1", "2"])
+def test_e2e_one_or_two_batches_in_flight(slots):
+    """The server's two staging slots (a batch's kernels and copies run while
+    the next batch is received; SRPC_SERVER_SLOTS=1: one at a time): the same
+    responses either way, foreign frames and poison included."""
+    n = 90_000
+    r = _run("--mode", "gpu", "--n", str(n), "--batch", "8192", "--port", str(18320 + int(slots)), "--mix",
+             "0.2", "--foreign", "0.02", "--poison", "0,8191,8192,89999", "--gpu-methods", "all", slots=slots)
+    g = _served(r, n)
+    t = r["traffic"]
+    assert g["fallback_requests"] == t["divide"] + t["poison"] and t["poison"] == 4
+    assert g["batches"] >= 10
 
 
 @pytest.mark.parametrize("at", [0, 3000])

@@ -156,6 +156,37 @@ def test_aos_unpack_into_fresh_objects(n, schema, envelope, vptr, shift):
     assert host(t, n * stride + 32)[shift + n * stride:].tobytes() == b"\xa5" * (32 - shift)
 
 
+@pytest.mark.parametrize("schema", ["pair", "i64x3", "i64x4", "quad"])
+def test_aos_run_unpack_refuses_wire_8_bytes_off_16(schema):
+    """the run layouts' whole-line piece unpack loads the wire
+    in 16-byte pieces.  A wire 8 bytes off 16-byte alignment never reaches it:
+    both AoS unpack entry points refuse it (SRPC_E_ALIGN) before any launch,
+    and the piece kernel's own dispatch requires a 16-byte aligned wire too;
+    the aligned wire of the same batch decodes exactly."""
+    kinds = {"quad": [oracle.INT32] * 4, "pair": [oracle.INT32] * 2, "i64x3": [oracle.INT64] * 3,
+             "i64x4": [oracle.INT64] * 4}[schema]
+    p = GpuPacker(Schema("S", tuple((f"f{i}", k) for i, k in enumerate(kinds))))
+    n = 4099
+    rng = np.random.default_rng(n + 77)
+    recs = random_records(kinds, n, rng, True)
+    stride, offs = layout(recs, len(kinds))
+    cols = [np.ascontiguousarray(recs[f"f{i}"]) for i in range(len(kinds))]
+    want = bytes(oracle.pack(kinds, cols, n))
+    w = empty(len(want) + 32)
+    w[8:8 + len(want)].copy_(torch.from_numpy(np.frombuffer(want, np.uint8).copy()))
+    d_other = dev(random_records(kinds, n, np.random.default_rng(3 + n), True).view(np.uint8))
+    fill = rng.integers(0, 256, stride, dtype=np.uint8).tobytes()
+    with pytest.raises(srpc_amd.SrpcError, match="misaligned"):
+        p.unpack_aos(w[8:], len(want), n, d_other, stride, offs)
+    with pytest.raises(srpc_amd.SrpcError, match="misaligned"):
+        p.unpack_aos_fill(w[8:], len(want), n, d_other, stride, offs, fill)
+    st = status_buf()
+    assert p.unpack_aos(dev(np.frombuffer(want, np.uint8)), len(want), n, d_other, stride, offs, st) == 0
+    back = host(d_other, n * stride).view(recs.dtype)
+    for i in range(len(kinds)):
+        assert back[f"f{i}"].tobytes() == recs[f"f{i}"].tobytes(), i
+
+
 def test_aos_all_kinds_reference_fixture(golden_dir):
     """The reference-built all_kinds.bin from structs instead of columns."""
     z = np.load(os.path.join(golden_dir, "all_kinds_in.npz"))
