@@ -61,9 +61,33 @@ constexpr uint32_t kSB = 8192;                   // wire bytes per block (one wo
 constexpr uint32_t kSC = kSB / kBlock;           // 32: wire bytes per speculating lane
 static_assert(kSC % 16 == 0 && kSC <= 64, "16-byte window reads; a chunk's positions fit one 64-bit mask");
 constexpr uint32_t kMargin = 1536;               // staged bytes past the block
+// Landing slots (round 5): the table also holds a slot at the end of every
+// record that starts in the kPre bytes before the block (its premargin) and
+// ends in the block past the window -- the true entry of a record that
+// straddles the block's start by up to kPre bytes, whatever the speculation
+// made of the block.  Wave 0 finds them alone, from the premargin staged
+// with the block, while waves 1-3 have left (no barrier,
+// nothing read from global memory; a first version that scanned with the
+// whole workgroup cost every random row 25-30 %, one that read the premargin
+// from global memory 10-23 %: profiles/r05_sdx_ab.log).  A/B build
+// SRPC_SX_NOLAND leaves them out.
+#ifndef SRPC_SX_NOLAND
+constexpr uint32_t kPre = 1024;                  // premargin: bytes before the block scanned for landings
+#else
+constexpr uint32_t kPre = 0;
+#endif
 constexpr uint32_t kStage = kSB + kMargin + 32;  // + 16-byte alignment slack on both sides
+constexpr uint32_t kStageS = kPre + kStage;      // phase 1's stage: the premargin, the block, the margin
 constexpr uint32_t kWin = 64;                    // entry window of a block's table (a lane per position)
-constexpr uint32_t kEnt = kWin + 1;              // table entries per block: the window's, then the extra slot
+#ifndef SRPC_SX_NOLAND
+constexpr uint32_t kX = 128;                     // landing slots per block
+#else
+constexpr uint32_t kX = 0;
+#endif
+constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
+constexpr uint32_t kEnt = kWin + 1 + kX;         // table entries per block: the window's, the extra slot,
+                                                 // then the landing slots
+constexpr uint32_t kHdr = 8;                     // header words per block
 constexpr uint32_t kGroup = 64;                  // blocks per group of the scan (a lane per block)
 constexpr int kMaxNC = 3;                        // chars values carried per state (string fields 0..ns-2)
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
@@ -77,6 +101,7 @@ constexpr int kKeep = 4;                         // table entries per block the 
 constexpr uint64_t kCnt40 = (1ull << 40) - 1;
 constexpr uint32_t kNoPrim = 0xFF;
 constexpr uint32_t kListCap = 4;                 // record starts a 32-byte chunk holds (records >= 8 bytes apart)
+static_assert(kSB / 32 == kBlock && kListCap == 4, "a lane per landing-bitmap word, over its own list entries");
 constexpr uint32_t kDead = 0x81;                 // stop bits of a group-table chain given up (k_sx_groups)
 
 // control words (scratch; k_sx_spec block 0 zeroes them each call)
@@ -113,11 +138,17 @@ __device__ unsigned long long g_sxph_blocks = 0;
     do {                                                                                           \
         if (blockIdx.x < g_sxph_blocks) g_sxph[static_cast<uint64_t>(blockIdx.x) * 16 + (i)] = (v);    \
     } while (0)
+#define SXP_ADD(i, v)                                                                              \
+    do {                                                                                           \
+        if (blockIdx.x < g_sxph_blocks) atomicAdd(g_sxph + static_cast<uint64_t>(blockIdx.x) * 16 + (i), \
+                                                  static_cast<unsigned long long>(v));              \
+    } while (0)
 #else
 #define SXP_BEGIN
 #define SXP(i)
 #define SXP_FLAG(i)
 #define SXP_SET(i, v)
+#define SXP_ADD(i, v)
 #endif
 
 typedef const uint8_t __attribute__((address_space(1))) global_u8;
@@ -156,6 +187,7 @@ struct SxScratch {
     uint64_t* bst;   // per block: the cursor's state where the block starts (E words)
     uint64_t* ctl;   // kCtlWords
     uint16_t* rl;    // per block, kMaxRec slots: its chunks' record starts in order (offsets from the block)
+    uint16_t* xp;    // per block, kX slots: its landing slots' positions (offsets from the block, ascending)
 };
 
 // A chain's result / the cursor's state: position (exit, or the next record
@@ -706,7 +738,8 @@ __device__ St<NC> walk_global(const SxArgs& a, const uint8_t* w, uint64_t x, uin
 
 // Slot of position x in a block's table (header words h0 = window mask, h1 =
 // the first speculated start, h3 = the first speculated start past the
-// window): its compact index (kWin for the extra slot), or -1 (a miss).
+// window): its compact index (kWin for the extra slot), or -1 (not one of
+// these; the landing slots are looked up by find_slot).
 __device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint64_t h3, uint32_t nslots, uint64_t b0,
                                        uint64_t x) {
     const uint64_t off = x - b0;
@@ -715,14 +748,75 @@ __device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint64_t h3, ui
     return x == h3 ? static_cast<int>(kWin) : -1;
 }
 
+// Header word 4: landing slots, their overflow, the block's first nonzero byte.
+__device__ __forceinline__ uint32_t h4_nx(uint64_t h4) { return static_cast<uint32_t>(h4 & 0xff); }
+__device__ __forceinline__ uint32_t h4_zr(uint64_t h4) { return static_cast<uint32_t>((h4 >> 16) & 0xffff); }
+__device__ __forceinline__ uint32_t h4_za(uint64_t h4) { return static_cast<uint32_t>((h4 >> 32) & 0xff); }
+
+// Where the cursor at x goes through block blk: the table entry `idx` (its
+// chain to the block's end), minus `sub` zero records (below), or idx < 0 (a
+// miss).  Beyond slot_of:
+// - the landing slots (xs: the block's ascending offsets, staged in LDS by
+//   the caller; a binary search per lane);
+// - a run of zero bytes: when the block's bytes [za, x) are all zero (za:
+//   just past the window's last nonzero byte, header word 4), the schema has
+//   no prefix and its all-zero record (fixed_bytes = Z long, every string
+//   empty) is at most kWin bytes, the window position w = za + (x - za) mod Z
+//   parses as zero records up to x -- so w's chain passes through x and the
+//   chain from x is w's without its first (x - w) / Z records (no chars).  A
+//   record whose chars are zeros and that straddles the block's start ends
+//   there, whatever its length (its length field may lie in the window).
+struct Slot {
+    int idx;
+    uint32_t sub;
+};
+__device__ __forceinline__ Slot find_slot(const SxArgs& a, uint64_t h0, uint64_t h1, uint64_t h3, uint32_t meta,
+                                          uint64_t h4, const uint16_t* xs, uint64_t b0, uint64_t x) {
+    Slot r{slot_of(h0, h1, h3, meta & 0xff, b0, x), 0};
+    if (r.idx >= 0 || (a.mode & 3)) return r;
+    const uint64_t off = x - b0;
+    const uint32_t nx = kX ? h4_nx(h4) : 0;
+    if (kX && nx && off < kSB) {
+        uint32_t lo = 0, hi = nx;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (xs[m] < off) lo = m + 1;
+            else hi = m;
+        }
+        if (lo < nx && xs[lo] == off) {
+            r.idx = static_cast<int>(kWin + 1 + lo);
+            return r;
+        }
+    }
+    const uint32_t Z = a.fixed_bytes, za = h4_za(h4);
+    if (!a.prefix_len && Z <= kWin && off >= za && off <= h4_zr(h4)) {
+        const uint32_t wo = za + static_cast<uint32_t>((off - za) % Z);
+        if (wo < kWin && ((h0 >> wo) & 1)) {
+            r.idx = __builtin_popcountll(h0 & ((1ull << wo) - 1));
+            r.sub = static_cast<uint32_t>((off - wo) / Z);
+        }
+    }
+    return r;
+}
+
+// The wave's LDS copy of block blk's landing slots (wave-uniform blk; every
+// lane takes part).
+__device__ __forceinline__ void stage_xs(const SxScratch& S, uint64_t blk, uint32_t nx, uint16_t* xs) {
+    if constexpr (kX == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = lane; i < nx; i += 64) xs[i] = S.xp[blk * kX + i];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // Prologue shared by the speculation and the decode: the prefix and the
-// block's bytes [b0, min(b1 + kMargin, W)) in LDS (LDS-DMA), then a barrier.
+// block's bytes [b0 - pre, min(b1 + kMargin, W)) in LDS (LDS-DMA), then a barrier.
 __device__ __forceinline__ StagedRd stage_block(const SxArgs& a, const uint8_t* w, uint8_t* st, uint8_t* pre,
-                                                uint64_t b0, uint64_t b1) {
+                                                uint64_t b0, uint64_t b1, uint32_t before = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     for (uint32_t i = tid; i < a.prefix_len + 16; i += kBlock) pre[i] = i < a.prefix_len ? a.prefix[i] : 0;
+    const uint64_t lo = b0 > before ? b0 - before : 0;
     const uint64_t hi = min<uint64_t>(b1 + kMargin, a.W);
-    const uint64_t A = (reinterpret_cast<uint64_t>(w) + b0) & ~15ull;
+    const uint64_t A = (reinterpret_cast<uint64_t>(w) + lo) & ~15ull;
     const uint32_t ng = static_cast<uint32_t>((reinterpret_cast<uint64_t>(w) + hi - A + 15) >> 4);
     for (uint32_t w0 = tid & ~63u; w0 < ng; w0 += kBlock) {
         const uint32_t gi = w0 + lane;
@@ -733,7 +827,7 @@ __device__ __forceinline__ StagedRd stage_block(const SxArgs& a, const uint8_t* 
         }
     }
     __syncthreads();  // waits for the LDS-DMA and publishes the stage
-    return StagedRd{(global_u8*)w, (lds_u8c*)st, A - reinterpret_cast<uint64_t>(w), b0, hi, (lds_u8c*)pre};
+    return StagedRd{(global_u8*)w, (lds_u8c*)st, A - reinterpret_cast<uint64_t>(w), lo, hi, (lds_u8c*)pre};
 }
 
 // Chunk tid's records from its start sp (or none): count, the position after
@@ -792,25 +886,214 @@ __device__ __forceinline__ void link_chunks(Chunks<NC>& L, uint64_t b0, uint64_t
     __syncthreads();
 }
 
+// Workgroup i -> block.  Dispatch order by default; with SRPC_SX_XCD the
+// dispatcher's round robin over the 8 XCDs (i mod 8, each with its own L2)
+// gives XCD x one contiguous run of blocks, so the bytes a block stages past
+// its end (and the next one's premargin) would be found in that XCD's L2 the
+// second time -- measured 1-3 % slower on every random row (the kernels are
+// not bound by those re-reads: profiles/r05_sdx_ab.log), so not the default.
+__device__ __forceinline__ uint64_t xcd_block(uint32_t i, uint32_t G) {
+#ifndef SRPC_SX_XCD
+    return i;
+#endif
+    const uint32_t x = i & 7, k = i >> 3, q = G >> 3, r = G & 7;
+    return static_cast<uint64_t>(x) * q + min(x, r) + k;
+}
+
 // ---- phase 1: speculation and the block tables ----------------------------------
 template <int NC>
 struct SpecLds {
-    alignas(16) uint8_t st[kStage + 16];  // wire bytes [base, base + kStage)
+    alignas(16) uint8_t st[kStageS + 16];  // wire bytes [base, base + kStageS)
     alignas(16) uint8_t pre[kMaxPrefix + 16];
     Chunks<NC> c;
-    uint8_t list[kBlock * kListCap];       // per chunk: its records' starts (offsets in the chunk)
+    // per chunk: its records' starts (offsets in the chunk); then wave 0's
+    // part (the record list written out) holds the landing slots
+    alignas(4) uint8_t list[kBlock * kListCap];
+    uint32_t s_nx;  // landings found (wave 0's counter)
 };
+static_assert(64 * kListCap >= 2 * kX, "the landing slots fit wave 0's part of the chunk lists");
 
+// Wave 1 of k_sx_spec: the block's zero run and landing slots (their chains
+// to the block's end and their positions), header word 4.
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+__device__ __forceinline__ void land_slots(const SxArgs& a, const StagedRd& rd, const StageOnlyRd& so,
+                                           const SxScratch& S, SpecLds<NC>& L, Chunks<NC>& C, uint64_t b,
+                                           uint64_t b0, uint64_t b1, uint64_t sF2) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t W = a.W;
+    // The zero run the window ends in (find_slot's zero-run rule, for schemas
+    // with no prefix whose all-zero record is at most kWin bytes): za = just
+    // past the window's last nonzero byte, zr = the first nonzero byte from
+    // there on -- bytes [za, zr) of the block are zero.
+    uint32_t za = 0, zr = 0;
+    if (!(a.mode & 3) && b > 0 && !a.prefix_len && a.fixed_bytes <= kWin) {
+        const uint32_t wofs = static_cast<uint32_t>(b0 - rd.base), blen = static_cast<uint32_t>(b1 - b0);
+        const uint64_t nz = __ballot(lane < blen && L.st[wofs + lane] != 0);
+        za = nz ? 64 - __builtin_clzll(nz) : 0;
+        zr = za;
+        if (za + a.fixed_bytes <= kWin) {  // a congruent window position can lie in the run
+            zr = blen;
+            for (uint32_t o = kWin; o < blen; o += 256) {  // a dword per lane from o on
+                const uint32_t p4 = o + 4 * lane;
+                uint32_t v = 0;
+                if (p4 < blen) {
+                    lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)L.st + ((wofs + p4) & ~3u));
+                    const uint32_t sh = (wofs + p4) & 3;
+                    v = sh ? __builtin_amdgcn_alignbyte(q[1], q[0], sh) : q[0];
+                    if (blen - p4 < 4) v &= (1u << (8 * (blen - p4))) - 1;
+                }
+                const uint64_t m = __ballot(v != 0);
+                if (m) {
+                    const uint32_t l0 = __builtin_ctzll(m);
+                    const uint32_t v0 = __builtin_amdgcn_readlane(v, l0);
+                    zr = o + 4 * l0 + (__builtin_ctz(v0) >> 3);
+                    break;
+                }
+            }
+        }
+    }
+    // The landing slots: the end q of every record that parses at a position
+    // p of the premargin [b0 - kPre, b0) and ends in the block past the
+    // window, where a record parses too (not at sF2, the extra slot).  Lane l
+    // takes positions p0 .. p0 + 15.  On a wire under 4 GiB a length that
+    // fits has its four high bytes zero: the lane's first string lengths come
+    // from one window of stage dwords and only those positions are tested (as
+    // chunk_mask_z).  Wave 1's part of the chunk lists (read above) holds the
+    // ends, then sorted (a rank per entry; duplicates are harmless).
+    uint32_t nx = 0, xover = 0;
+    uint16_t* xl = reinterpret_cast<uint16_t*>(L.list + 64 * kListCap);  // wave 1's part
+#ifdef SRPC_SX_NOSCAN
+    if (false) {  // (A/B: the slots' layout and the premargin's staging without the scan)
+#else
+    if (kX && !(a.mode & 3) && b > 0) {
+#endif
+        const uint64_t p0 = b0 - kPre + 16 * lane;
+        uint32_t cand = 0xffff;
+        if (W < (1ull << 32) && a.first_len_at + 64 <= kMargin) {  // (the window's dwords lie in the stage)
+            const uint32_t o = static_cast<uint32_t>(p0 + a.first_len_at - rd.base);
+            lds_u32c* q = reinterpret_cast<lds_u32c*>((lds_u8c*)L.st + (o & ~3u));
+            uint32_t d[7];
+#pragma unroll
+            for (uint32_t k = 0; k < 7; ++k) d[k] = q[k];
+            const uint32_t sh = o & 3;  // (the same for every lane)
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            // and, from the same window, the record's end where it is fixed
+            // by the first length (one string, no prefix): in the block past
+            // the window; otherwise at least not past the block's end
+            const bool one = a.nstrings == 1 && !a.prefix_len;
+            const uint32_t rest = one ? a.fixed_bytes : a.first_len_at + 8;
+            const uint32_t off0 = kPre - 16 * lane, blen = static_cast<uint32_t>(b1 - b0);  // b0 - p0
+            cand = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) {  // bytes i + 4 .. i + 7 of the window zero
+                const uint32_t k = (i + 4) >> 2, s8 = (i + 4) & 3;
+                const uint32_t hi32 = s8 ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], s8) : d[k];
+                const uint32_t k0 = i >> 2, s0 = i & 3;
+                const uint32_t lo32 = s0 ? __builtin_amdgcn_alignbyte(d[k0 + 1], d[k0], s0) : d[k0];
+                // the end q - b0 = len + rest - (off0 - i) (a length of 2^24 or
+                // more ends past any block: clamped there, 32-bit arithmetic)
+                const int32_t e = static_cast<int32_t>(min(lo32, 1u << 24) + rest) - static_cast<int32_t>(off0 - i);
+                const bool ok = hi32 == 0 && e < static_cast<int32_t>(blen) && (!one || e >= static_cast<int32_t>(kWin));
+                cand |= (ok ? 1u : 0u) << i;
+            }
+            if (a.prefix_len) {  // the prefix's first (up to 4) bytes at p
+                const uint32_t po = static_cast<uint32_t>(p0 - rd.base);
+                lds_u32c* r = reinterpret_cast<lds_u32c*>((lds_u8c*)L.st + (po & ~3u));
+                uint32_t e5[6];
+#pragma unroll
+                for (uint32_t k = 0; k < 6; ++k) e5[k] = r[k];
+                const uint32_t sp = po & 3;  // (the same for every lane)
+#pragma unroll
+                for (uint32_t k = 0; k < 5; ++k) e5[k] = __builtin_amdgcn_alignbyte(e5[k + 1], e5[k], sp);
+                const uint32_t pk = a.prefix_len < 4 ? a.prefix_len : 4;
+                const uint32_t pm = pk == 4 ? ~0u : (1u << (8 * pk)) - 1, pv = static_cast<uint32_t>(a.pre8) & pm;
+                uint32_t mp = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 16; ++i) {
+                    const uint32_t k = i >> 2, s8 = i & 3;
+                    const uint32_t v = s8 ? __builtin_amdgcn_alignbyte(e5[k + 1], e5[k], s8) : e5[k];
+                    mp |= ((v & pm) == pv ? 1u : 0u) << i;
+                }
+                cand &= mp;
+            }
+        }
+        SXP_ADD(5, __builtin_popcount(cand));
+        while (cand) {
+            const uint32_t i = __builtin_ctz(cand);
+            cand &= cand - 1;
+            const uint64_t p = p0 + i;
+            if (!filter(a, rd, p)) continue;
+            uint64_t qe;
+            if (a.nstrings == 1 && !a.prefix_len) {
+                qe = p + a.fixed_bytes + rd.u64(p + a.first_len_at);
+            } else {
+                uint32_t err;
+                uint64_t t[kMaxNC + 1];
+                qe = parse_rd<0>(a, rd, p, &err, t);
+                if (err) continue;
+            }
+            SXP_ADD(6, qe >= b0 + kWin && qe < b1 && qe != sF2 ? 1 : 0);
+            if (qe >= b0 + kWin && qe < b1 && qe != sF2 && filter(a, so, qe) && plausible(a, rd, qe)) {
+                const uint32_t j = atomicAdd(&L.s_nx, 1u);
+                if (j < kX) xl[j] = static_cast<uint16_t>(qe - b0);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t tot = __builtin_amdgcn_readfirstlane(__atomic_load_n(&L.s_nx, __ATOMIC_RELAXED));
+        SXP_SET(7, tot);
+
+        nx = min(tot, kX);
+        xover = tot > kX ? 1u : 0u;
+        if (nx > 1) {
+            const uint32_t v0 = lane < nx ? xl[lane] : 0xffffu, v1 = lane + 64 < nx ? xl[lane + 64] : 0xffffu;
+            uint32_t r0 = 0, r1 = 0;
+            for (uint32_t k = 0; k < nx; ++k) {
+                const uint32_t v = xl[k];
+                r0 += v < v0 || (v == v0 && k < lane);
+                r1 += v < v1 || (v == v1 && k < lane + 64);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every read before the writes
+            if (lane < nx) xl[r0] = static_cast<uint16_t>(v0);
+            if (lane + 64 < nx) xl[r1] = static_cast<uint16_t>(v1);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+    }
+    for (uint32_t j = lane; j < nx; j += 64) {
+        const uint32_t o = xl[j];
+        st_store<NC>(S.ent + (b * kEnt + kWin + 1 + j) * ew<NC>(),
+                     walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
+        S.xp[b * kX + j] = static_cast<uint16_t>(o);
+    }
+    if (lane == 0)
+        S.hdr[kHdr * b + 4] = nx | (xover << 8) | (static_cast<uint64_t>(zr) << 16) | (static_cast<uint64_t>(za) << 32);
+}
+
+// k_sx_spec held to the registers of 8 waves per SIMD (56 VGPRs, no spill):
+// left to itself the compiler takes 64-68 and the kernel drops to 7 waves per
+// SIMD, 8 % slower on the random rows (profiles/r05_sdx_ab.log).  A/B builds
+// set SRPC_SX_WPE (0 = no hint).
+#ifndef SRPC_SX_WPE
+#define SRPC_SX_WPE 8
+#endif
+#if SRPC_SX_WPE
+// (the three-chars-states instance is held to 7 by its LDS: the hint stays a hint)
+#pragma clang diagnostic ignored "-Wpass-failed"
+#define SX_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(SRPC_SX_WPE, SRPC_SX_WPE)))
+#else
+#define SX_SPEC_ATTR
+#endif
+template <int NC>
+__global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
     __shared__ SpecLds<NC> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint64_t b = blockIdx.x;
+    const uint64_t b = xcd_block(blockIdx.x, gridDim.x);
     const uint64_t W = a.W;
     const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
     SXP_BEGIN
     if (b == 0 && tid < kCtlWords) S.ctl[tid] = 0;  // this call's counters (read by the later launches)
-    const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);
+    if (tid == 0) L.s_nx = 0;
+    const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1, kPre);
     const StageOnlyRd so{rd};
     SXP(0);
 
@@ -930,22 +1213,31 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     }
     SXP(2);
 
-    // the table (wave 0, lane = window position): every plausible position of
-    // the block's first kWin bytes; a window with none holds the first
-    // speculated start (sF) alone.  The primary slot is sF's: the entry the
-    // speculation itself predicts.  Wave 1 meanwhile adds the extra slot, the
-    // first speculated start past the window (a record longer than the window
-    // that ends where its chunk speculated: entered there, not walked).
-    if (tid >= 128) return;
-    if (tid >= 64) {
-        if (tid == 64) {
-            const uint32_t F2 = next_bit(C.has, kWin / kSC);
-            uint64_t sF2 = F2 < kBlock && b > 0 && !(a.mode & 3) ? b0 + C.start[F2] : ~0ull;
+    const uint32_t F2 = next_bit(C.has, kWin / kSC);
+    const uint64_t sF2 = F2 < kBlock && b > 0 && !(a.mode & 3) ? b0 + C.start[F2] : ~0ull;
+
+    // The table, three waves at once (the workgroup holds its LDS until the
+    // last of them is done: work added to one wave's share lengthens every
+    // block's life, and so the kernel, unless it overlaps another's).
+    // - wave 0 (lane = window position): every plausible position of the
+    //   block's first kWin bytes; a window with none holds the first
+    //   speculated start (sF) alone.  The primary slot is sF's: the entry the
+    //   speculation itself predicts.  Header words 0-2.
+    // - wave 1: the zero run and the landing slots, header word 4.
+    // - one lane of wave 3: the extra slot, the first speculated start past
+    //   the window (a record longer than the window that ends where its chunk
+    //   speculated: entered there, not walked), header word 3.
+    if (tid >= 128) {
+        if (tid == kBlock - 1) {
             if (sF2 != ~0ull)
                 st_store<NC>(S.ent + (b * kEnt + kWin) * ew<NC>(),
                              walk_chain<NC, false>(a, rd, C, b0, b1, sF2, nullptr, nullptr));
-            S.hdr[4 * b + 3] = sF2;
+            S.hdr[kHdr * b + 3] = sF2;
         }
+        return;
+    }
+    if (tid >= 64) {
+        land_slots<NC>(a, rd, so, S, L, C, b, b0, b1, sF2);
         return;
     }
     const uint32_t F = next_bit(C.has, 0);
@@ -954,8 +1246,11 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
     if (b == 0) {
         if (lane == 0) mycand = 0;
     } else if (!(a.mode & 3)) {
+        // (the records read through the stage or, for a record that runs past
+        // it, global memory: a true entry whose next record starts beyond the
+        // stage is a slot too, not a miss)
         const uint64_t p = b0 + lane;
-        if (p < b1 && filter(a, so, p) && plausible(a, so, p)) mycand = p;
+        if (p < b1 && filter(a, so, p) && plausible(a, rd, p)) mycand = p;
     }
     uint64_t wmask = __ballot(mycand != ~0ull);
     if (!wmask && lane == 0 && sF != ~0ull && !(a.mode & 2)) mycand = sF;
@@ -987,7 +1282,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
         }
         const bool one = sF != ~0ull && ntail == 1 && (C.stop[lastc] || C.exit[lastc] >= b1);
         SXP_SET(14, ntail);
-        uint64_t* h = S.hdr + 4 * b;
+        uint64_t* h = S.hdr + kHdr * b;
         h[0] = wmask;
         h[1] = sF;
         h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull) |
@@ -1004,7 +1299,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_spec(SxArgs a, const uint8_t* __r
 // the primary chains' records and chars (inclusive prefix sums over the lanes).
 template <int NC>
 struct Held {
-    uint64_t h0, h1, h3;
+    uint64_t h0, h1, h3, h4;
     uint32_t meta;  // slots | primary << 8
     uint64_t e[kKeep][ew<NC>()];
     bool has_prim;
@@ -1013,16 +1308,17 @@ struct Held {
     uint32_t run;                       // the last block of the run of primary links from this one
     __device__ __forceinline__ void load(const SxScratch& S, uint64_t blk, bool ok, uint32_t nbk) {
         const uint32_t lane = threadIdx.x & 63;
-        h0 = 0;
+        h0 = h4 = 0;
         h1 = h3 = ~0ull;
         meta = 0;
         has_prim = false;
         pe = St<NC>{};
         if (ok) {
-            const uint64_t* h = S.hdr + 4 * blk;
+            const uint64_t* h = S.hdr + kHdr * blk;
             h0 = h[0];
             h1 = h[1];
             h3 = h[3];
+            h4 = h[4];
             meta = static_cast<uint32_t>(h[2]);
             const uint32_t ns = meta & 0xff, prim = (meta >> 8) & 0xff;
 #pragma unroll
@@ -1080,12 +1376,13 @@ struct Held {
 // The cursor's state s through block blk (held in lane l of hv; uniform
 // across the wave or per lane), or, past the held entries, from scratch;
 // in no slot: walked from global memory.  *miss / *off count what happened.
+// xs: the wave's LDS room for the block's landing slots.
 template <int NC>
 __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w, const SxScratch& S,
                                               const Held<NC>& hv, uint32_t l, uint64_t blk, St<NC>& s, bool* miss,
-                                              bool* off, uint8_t* stage, bool may_walk = true) {
+                                              bool* off, uint8_t* stage, uint16_t* xs, bool may_walk = true) {
     // the held words of lane l (uniform reads, every lane takes part)
-    const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l), h3 = rl64(hv.h3, l);
+    const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l), h3 = rl64(hv.h3, l), h4 = rl64(hv.h4, l);
     const uint32_t meta = __builtin_amdgcn_readlane(hv.meta, l);
     uint64_t e[kKeep][ew<NC>()];
 #pragma unroll
@@ -1095,43 +1392,48 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
     const uint64_t b0 = blk * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
     // a block no record starts in (the cursor is past its end) passes the state on
     const bool act = !st_done(s, a.W) && s.x < b1;
-    const int idx = act ? slot_of(h0, h1, h3, meta & 0xff, b0, s.x) : 0;
-    const bool walk = act && idx < 0 && may_walk;
+    const uint32_t nx = h4_nx(h4);
+    if (nx && !(a.mode & 3) && __ballot(act)) stage_xs(S, blk, nx, xs);
+    const Slot sl = act ? find_slot(a, h0, h1, h3, meta, h4, xs, b0, s.x) : Slot{0, 0};
+    const bool walk = act && sl.idx < 0 && may_walk;
     // every lane of the wave takes part in the staging of walk_miss
     St<NC> mw{};
     if (__ballot(walk)) mw = walk_miss<NC>(a, w, stage, b0, b1, s.x, walk);
-    if (act && idx < 0 && !may_walk) {  // a chain the caller gives up on instead of walking it
+    if (act && sl.idx < 0 && !may_walk) {  // a chain the caller gives up on instead of walking it
         s.stop = kDead;
         return;
     }
     if (!act) return;
     St<NC> t;
-    if (idx >= 0 && idx < kKeep) {
+    if (sl.idx >= 0 && sl.idx < kKeep) {
         uint64_t v[ew<NC>()];
 #pragma unroll
         for (uint32_t j = 0; j < ew<NC>(); ++j) {
             v[j] = e[0][j];
 #pragma unroll
-            for (int k = 1; k < kKeep; ++k) v[j] = idx == k ? e[k][j] : v[j];
+            for (int k = 1; k < kKeep; ++k) v[j] = sl.idx == k ? e[k][j] : v[j];
         }
         t = st_load<NC>(v);
-    } else if (idx >= 0) {
-        t = st_load<NC>(S.ent + (blk * kEnt + idx) * ew<NC>());
+        t.cnt -= sl.sub;
+    } else if (sl.idx >= 0) {
+        t = st_load<NC>(S.ent + (blk * kEnt + sl.idx) * ew<NC>());
+        t.cnt -= sl.sub;
     } else {
         t = mw;
         *miss = true;
     }
-    if (idx != static_cast<int>((meta >> 8) & 0xff)) *off = true;
+    if (sl.idx != static_cast<int>((meta >> 8) & 0xff) || sl.sub) *off = true;
     st_add<NC>(s, t);
 }
 
-// A wave per group: for every slot of the group's first block, the chain
-// through the group's blocks (the group's table, compact in the first block's
-// slot order).  Only the primary slot's chain is walked where it meets no
-// slot; any other chain that does is given up (kDead): a start the block
-// speculated wrongly that runs into positions no table holds would otherwise
-// cost a walk in every later block, and the cursor enters a group there
-// rarely (k_sx_top then takes that group block by block).
+// A wave per group: for every slot of the group's first block -- window
+// slots, the extra slot, landing slots -- the chain through the group's blocks
+// (the group's table, indexed like the first block's).  Only the primary
+// slot's chain is walked where it meets no slot; any other chain that does is
+// given up (kDead): a start the block speculated wrongly that runs into
+// positions no table holds would otherwise cost a walk in every later block,
+// and the cursor enters a group there rarely (k_sx_top then takes that group
+// block by block).
 template <int NC>
 __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1141,36 +1443,48 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
     Held<NC> hv;
     hv.load(S, bf + lane, lane < nbk, nbk);
-    const uint32_t ns0 = __builtin_amdgcn_readlane(hv.meta, 0) & 0xff;
-    const bool act = lane < ns0;
-    St<NC> s{};
-    s.stop = 1;  // lanes past the slots stay put
-    if (act) s = st_load<NC>(S.ent + (bf * kEnt + lane) * ew<NC>());
-    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
-    uint8_t* stage = stages[threadIdx.x >> 6];
-    bool miss = false, off = false;
-    const bool primary = lane == ((__builtin_amdgcn_readlane(hv.meta, 0) >> 8) & 0xff);
-    for (uint32_t j = 1; j < nbk; ++j) {
-        // chains entering block j at its primary cross its whole run at once
-        const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
-        if (hp) hv.jump(j, s, act && !st_done(s, a.W) && s.x == rl64(hv.h1, j));
-        const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
-        if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
-        St<NC> t = s;
-        through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, primary);
-        if (act) s = t;
-    }
-    if (act) st_store<NC>(S.gent + (g * kWin + lane) * ew<NC>(), s);
-    // what the in-order pass over the groups reads first, in one record
-    uint64_t* q = S.gp + g * (4 + ew<NC>());
     const uint32_t meta0 = __builtin_amdgcn_readlane(hv.meta, 0);
-    if (lane == 0) {
-        q[0] = rl64(hv.h0, 0);
-        q[1] = rl64(hv.h1, 0);
-        q[2] = meta0;
-        q[3] = rl64(hv.h3, 0);
+    const uint32_t ns0 = meta0 & 0xff, prim0 = (meta0 >> 8) & 0xff;
+    const bool has3 = rl64(hv.h3, 0) != ~0ull;
+    const uint32_t nx0 = (a.mode & 3) ? 0 : h4_nx(rl64(hv.h4, 0));
+    const uint32_t total = ns0 + (has3 ? 1 : 0) + nx0;
+    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    __shared__ uint16_t xss[kBlock / 64][kXA];
+    uint8_t* stage = stages[threadIdx.x >> 6];
+    uint16_t* xs = xss[threadIdx.x >> 6];
+    bool miss = false, off = false;
+    uint64_t* q = S.gp + g * (kHdr + ew<NC>());
+    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+        // lane -> slot index: window slots, then the extra slot, then the landing slots
+        const uint32_t k = k0 + lane;
+        const bool act = k < total;
+        uint32_t idx = k;
+        if (k >= ns0) idx = has3 && k == ns0 ? kWin : kWin + 1 + (k - ns0 - (has3 ? 1 : 0));
+        St<NC> s{};
+        s.stop = 1;  // lanes past the slots stay put
+        if (act) s = st_load<NC>(S.ent + (bf * kEnt + idx) * ew<NC>());
+        const bool primary = act && idx == prim0;
+        for (uint32_t j = 1; j < nbk; ++j) {
+            // chains entering block j at its primary cross its whole run at once
+            const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
+            if (hp) hv.jump(j, s, act && !st_done(s, a.W) && s.x == rl64(hv.h1, j));
+            const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
+            if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
+            St<NC> t = s;
+            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, xs, primary);
+            if (act) s = t;
+        }
+        if (act) st_store<NC>(S.gent + (g * kEnt + idx) * ew<NC>(), s);
+        if (primary) st_store<NC>(q + kHdr, s);  // what the in-order pass reads first
     }
-    if (act && lane == ((meta0 >> 8) & 0xff)) st_store<NC>(q + 4, s);
+    // the first block's header words, with the primary chain above: one record
+    if (lane < 5) {
+        const uint64_t hw[5] = {rl64(hv.h0, 0), rl64(hv.h1, 0), meta0, rl64(hv.h3, 0), rl64(hv.h4, 0)};
+        uint64_t v = hw[0];
+#pragma unroll
+        for (uint32_t i = 1; i < 5; ++i) v = lane == i ? hw[i] : v;
+        q[lane] = v;
+    }
 }
 
 // One wave: the groups in order.  Each group's entry state (the cursor where
@@ -1183,26 +1497,28 @@ template <int NC, bool kDecode>
 __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
                                                srpc_unpack_status* st) {
     constexpr uint32_t E = ew<NC>();
+    constexpr uint32_t R = kHdr + E;  // words of a group's record in S.gp
     const uint32_t lane = threadIdx.x;
     const uint64_t W = a.W;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
+    __shared__ uint16_t xs[kXA];
     St<NC> s{};
     bool miss = false, off = false;
     // lane l: group base + l -- its first block's header and the group's
     // primary entry (S.gp), the next batch's loaded while this one is walked
-    uint64_t nq[4 + E];
+    uint64_t nq[R];
     auto fetch = [&](uint64_t base) {
         const uint64_t g = base + lane;
 #pragma unroll
-        for (uint32_t j = 0; j < 4 + E; ++j) nq[j] = g < a.ng ? S.gp[g * (4 + E) + j] : 0;
+        for (uint32_t j = 0; j < R; ++j) nq[j] = g < a.ng && (j < 5 || j >= kHdr) ? S.gp[g * R + j] : 0;
     };
     fetch(0);
     for (uint64_t base = 0; base < a.ng; base += 64) {
         const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(64, a.ng - base));
         const uint64_t g = base + lane;
-        const uint64_t h0 = nq[0], h1 = nq[1], h3 = nq[3];
+        const uint64_t h0 = nq[0], h1 = nq[1], h3 = nq[3], h4 = nq[4];
         const uint32_t meta = static_cast<uint32_t>(nq[2]);
-        St<NC> pe = st_load<NC>(nq + 4);  // the group's chain from its primary slot (its first block's sF = h1)
+        St<NC> pe = st_load<NC>(nq + kHdr);  // the group's chain from its primary slot (its first block's sF = h1)
         fetch(base + 64);
         const bool has_prim = lane < cnt && ((meta >> 8) & 0xff) != kNoPrim;
         // link k -> k + 1: group k's primary chain enters group k + 1 at its primary
@@ -1228,7 +1544,7 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
         uint32_t l = 0;
         while (l < cnt) {
             const uint64_t gl = base + l;
-            const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l), lh3 = rl64(h3, l);
+            const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l), lh3 = rl64(h3, l), lh4 = rl64(h4, l);
             const uint32_t lmeta = __builtin_amdgcn_readlane(meta, l);
             const uint32_t lprim = (lmeta >> 8) & 0xff;
             if (!st_done(s, W) && lprim != kNoPrim && s.x == lh1) {
@@ -1273,26 +1589,34 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
             const uint64_t bend = min<uint64_t>(bf + kGroup, a.nb);
             if (s.x >= min<uint64_t>(bend * kSB, W)) continue;  // the whole group lies inside one record
             const uint64_t blk = s.x / kSB;
-            int idx = -1;
-            if (blk == bf) idx = slot_of(lh0, lh1, lh3, lmeta & 0xff, bf * kSB, s.x);
-            if (idx >= 0 && idx < static_cast<int>(kWin)) {  // (no group-table entry for the extra slot)
-                const St<NC> e = st_load<NC>(S.gent + (gl * kWin + idx) * E);
-                if (e.stop != kDead) {  // (the primary slot's is taken above)
-                    off = true;
-                    st_add<NC>(s, e);
-                    continue;
+            if (blk == bf) {
+                const uint32_t nx = h4_nx(lh4);
+                if (nx && !(a.mode & 3)) stage_xs(S, bf, nx, xs);
+                const Slot sl = find_slot(a, lh0, lh1, lh3, lmeta, lh4, xs, bf * kSB, s.x);
+                if (sl.idx >= 0) {
+                    St<NC> e = st_load<NC>(S.gent + (gl * kEnt + sl.idx) * E);
+                    if (e.stop != kDead) {  // (the primary slot's is taken above)
+                        off = true;
+                        e.cnt -= sl.sub;
+                        st_add<NC>(s, e);
+                        continue;
+                    }
                 }
             }
             // block by block from the cursor's block to the group's end
             for (uint64_t j = blk; j < bend && !st_done(s, W); ++j) {
                 const uint64_t b0 = j * kSB, b1 = min<uint64_t>(b0 + kSB, W);
                 if (s.x >= b1) continue;
-                const uint64_t* h = S.hdr + 4 * j;
-                const uint64_t m = h[2];
-                const int k = slot_of(h[0], h[1], h[3], static_cast<uint32_t>(m & 0xff), b0, s.x);
-                if (k != static_cast<int>((m >> 8) & 0xff)) off = true;
-                if (k >= 0) {
-                    st_add<NC>(s, st_load<NC>(S.ent + (j * kEnt + k) * E));
+                const uint64_t* h = S.hdr + kHdr * j;
+                const uint64_t m = h[2], hj4 = h[4];
+                const uint32_t nx = h4_nx(hj4);
+                if (nx && !(a.mode & 3)) stage_xs(S, j, nx, xs);
+                const Slot sl = find_slot(a, h[0], h[1], h[3], static_cast<uint32_t>(m), hj4, xs, b0, s.x);
+                if (sl.idx != static_cast<int>((m >> 8) & 0xff) || sl.sub) off = true;
+                if (sl.idx >= 0) {
+                    St<NC> t = st_load<NC>(S.ent + (j * kEnt + sl.idx) * E);
+                    t.cnt -= sl.sub;
+                    st_add<NC>(s, t);
                 } else {
                     st_add<NC>(s, walk_miss<NC>(a, w, stage, b0, b1, s.x, true));
                     miss = true;
@@ -1358,7 +1682,9 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
     St<NC> s = st_load<NC>(S.gin + g * E);
     uint64_t out[E];
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    __shared__ uint16_t xss[kBlock / 64][kXA];
     uint8_t* stage = stages[threadIdx.x >> 6];
+    uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     for (uint32_t j = 0; j < nbk;) {
         const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
@@ -1388,7 +1714,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
         st_store<NC>(v, s);
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) out[k] = lane == j ? v[k] : out[k];
-        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage);
+        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage, xs);
         ++j;
     }
     if (lane < nbk)
@@ -1426,7 +1752,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
     __shared__ DecLds<NC> L;
     constexpr uint32_t E = ew<NC>();
     const uint32_t tid = threadIdx.x;
-    const uint64_t b = blockIdx.x;
+    const uint64_t b = xcd_block(blockIdx.x, gridDim.x);
     const uint64_t W = a.W, n = a.n;
     // the tail: records T + 1 .. n when the stream stopped before record n
     if (S.ctl[kCtlTailOn]) {
@@ -1449,7 +1775,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
     // flight at once (a block no record of the batch starts in wastes its stage)
     SXP_BEGIN
     const St<NC> s = st_load<NC>(S.bst + b * E);
-    const uint64_t hsF = S.hdr[4 * b + 1], hmeta = S.hdr[4 * b + 2];
+    const uint64_t hsF = S.hdr[kHdr * b + 1], hmeta = S.hdr[kHdr * b + 2];
     const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
     const uint8_t sb = clo < b1 ? S.spec[b * kBlock + tid] : kNoSpec;
     // the record list's first 256 entries (the fast path's, read before it is
@@ -1751,7 +2077,7 @@ __global__ void k_zero_ctl(uint64_t* ctl) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct SxLayout {
-    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, total;
+    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, xp, total;
 };
 
 SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
@@ -1763,13 +2089,13 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     L.spec = o;
     o += r256(L.nb * kBlock);
     L.hdr = o;
-    o += r256(8 * 4 * L.nb);
+    o += r256(8 * kHdr * L.nb);
     L.ent = o;
     o += r256(8 * E * kEnt * L.nb);
     L.gent = o;
-    o += r256(8 * E * kWin * L.ng);
+    o += r256(8 * E * kEnt * L.ng);
     L.gp = o;
-    o += r256(8 * (4 + E) * L.ng);
+    o += r256(8 * (kHdr + E) * L.ng);
     L.gin = o;
     o += r256(8 * E * L.ng);
     L.bst = o;
@@ -1778,6 +2104,8 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     o += r256(8 * kCtlWords);
     L.rl = o;
     o += r256(2 * kMaxRec * L.nb);
+    L.xp = o;
+    o += r256(2 * kX * L.nb);
     L.total = o;
     return L;
 }
@@ -1844,7 +2172,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
                 reinterpret_cast<uint64_t*>(base + SL.gin),
                 reinterpret_cast<uint64_t*>(base + SL.bst),
                 reinterpret_cast<uint64_t*>(base + SL.ctl),
-                reinterpret_cast<uint16_t*>(base + SL.rl)};
+                reinterpret_cast<uint16_t*>(base + SL.rl),
+                reinterpret_cast<uint16_t*>(base + SL.xp)};
     SxArgs a{};
     uint32_t si = 0;
     for (uint32_t f = 0; f < p->nfields; ++f) {

@@ -38,6 +38,7 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover - CPU container
     pytest.skip("no GPU", allow_module_level=True)
 
+from tests.streams import straddler_stream as _straddler_stream  # noqa: E402
 from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty, host, read_status, status_buf  # noqa: E402
 
 RES_OFF, RES_MISS = 1, 2  # srpc_unpack_status.reserved bits (srpc_gpu.h)
@@ -307,9 +308,11 @@ def test_adversarial_streams_at_scale(n, schema, path):
 @pytest.mark.parametrize("n", [300, 3000])
 def test_long_zero_strings_entries_no_block_guesses(n, path):
     """Strings of 0-20000 zero bytes: inside one every position parses as an
-    empty record, so a block's candidates are all wrong and the record end
-    that enters it is found only from its predecessor's state (the miss path:
-    the block walks from its entry).  Exact, and each miss is counted."""
+    empty record, so a block's candidates are all wrong.  In the library's
+    tables the record end that enters such a block is found by the zero-run
+    rule (the window position congruent to it modulo the 8-byte empty record
+    passes through it: no walk); with the test hook's tables it is walked
+    from the block's entry, and each miss is counted.  Exact either way."""
     kinds = [oracle.STRING]
     rng = np.random.default_rng(n)
     lens = rng.integers(0, 20000, n).astype(np.uint64)
@@ -321,8 +324,42 @@ def test_long_zero_strings_entries_no_block_guesses(n, path):
     rec = check_clean(p, kinds, wire, n)
     assert np.array_equal(rec, _rec_offsets(kinds, [o], n))
     r = stream_unpack.last_reserved
-    if n >= 3000:
+    if path == "tables":
+        assert r >> 8 == 0, r  # no block walked
+    elif n >= 3000:
         assert r & RES_MISS and r >> 8 > 0, r
+
+
+ZH4 = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
+
+
+
+@pytest.mark.parametrize("n,lead,over,fill", [
+    (1 << 22, (1, 960), (65, 1000), "zero"),    # the verdict's stream at 4M records
+    (1 << 20, (1, 6000), (65, 6000), "zero"),   # straddlers of up to 12 KiB
+    (1 << 16, (1, 960), (65, 1000), "zero"),
+    (1 << 16, (1, 900), (65, 100), "heavy")])   # zero-heavy straddlers: the residual (walked)
+def test_straddling_records_at_every_block(n, lead, over, fill, path):
+    """a record straddles EVERY 8 KiB boundary and
+    ends past the block's window, where no speculated start is.  Records of
+    zero bytes (the verdict's stream), whatever their length, are found by
+    the zero-run rule -- nothing is walked in the library's tables mode
+    (reserved >> 8 == 0).  Straddlers with zero-heavy chars are the residual
+    case: their blocks are walked, serially.  Exact in every
+    mode."""
+    if path != "tables" and n > 1 << 16:
+        pytest.skip("tables with no slots walk every block: covered at 64K records")
+    rng = np.random.default_rng(n + lead[1] + over[1] + len(fill))
+    cols, offs = _straddler_stream(n, rng, lead, over, fill)
+    p = GpuPacker(Schema("Z", tuple((f"f{i}", k) for i, k in enumerate(ZH4))))
+    wire = oracle.pack(ZH4, cols, n, b"", offs)
+    rec = check_clean(p, ZH4, wire, n)
+    assert np.array_equal(rec, _rec_offsets(ZH4, offs, n))
+    r = stream_unpack.last_reserved
+    if path == "tables" and fill == "zero":
+        assert r >> 8 == 0, (r >> 8, len(wire) // 8192)
+    elif path != "tables" and len(wire) > 64 * 8192:
+        assert r & RES_MISS, r
 
 
 def test_records_across_block_edges_and_margin(path):

@@ -176,6 +176,16 @@ def main():
     case("zh4_zero_heavy_4M", zh, 1 << 22, gen_zero_heavy)
     case("multiple_primitives_zeros_4M", mp, 1 << 22,
          lambda k, n, r: gen_zero_heavy(k, n, r, maxlen=1, p_empty=1.0, p_nonzero=0.0))
+    # a record straddling EVERY 8 KiB boundary, ending
+    # past the block's window (tests/streams.py)
+    from tests.streams import straddler_stream
+    case("zh4_straddle_zero_4M", zh, 1 << 22, lambda k, n, r: straddler_stream(n, r, (1, 960), (65, 1000), "zero"))
+    case("zh4_straddle_zero_long_4M", zh, 1 << 22,
+         lambda k, n, r: straddler_stream(n, r, (1, 6000), (65, 6000), "zero"))
+    case("zh4_straddle_heavy_4M", zh, 1 << 22, lambda k, n, r: straddler_stream(n, r, (1, 900), (65, 100), "heavy"))
+    # the residual: zero-heavy straddlers that start more than kPre before the boundary
+    case("zh4_straddle_heavy_long_256K", zh, 1 << 18,
+         lambda k, n, r: straddler_stream(n, r, (1100, 4000), (65, 1000), "heavy"))
     if args.out:
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:

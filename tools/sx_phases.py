@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SPEC = ["stage", "speculate+walk", "link", "table"]
+SPEC = ["stage", "speculate+walk", "link", "chains+header", "window+landing scan"]
 DEC = ["stage+state", "chunk walk", "link", "chain+list", "fixed fields", "strings"]
 
 
@@ -71,12 +71,14 @@ def main():
         torch.cuda.synchronize()
         assert hook(None, 0) == 0
         b = buf.cpu().numpy().reshape(nb, 16).astype(np.float64)
-        spec = b[:, 0:4]
+        spec = b[:, 0:5]
         dec = b[:, 8:14]
         ran = dec.sum(1) > 0
         print(f"{name}: {nb} blocks, {int(ran.sum())} decoded")
         print("  k_sx_spec   " + "  ".join(f"{k} {v:8.0f}" for k, v in zip(SPEC, spec.mean(0))) +
               f"   total {spec.sum(1).mean():8.0f} cycles/block")
+        print(f"  landing scan per block: candidates {b[:, 5].mean():.1f}, ends past the window {b[:, 6].mean():.1f}, "
+              f"slots {b[:, 7].mean():.2f} (blocks with any {np.mean(b[:, 7] > 0):.3f}, max {b[:, 7].max():.0f})")
         print("  k_sx_decode " + "  ".join(f"{k} {v:8.0f}" for k, v in zip(DEC, dec[ran].mean(0))) +
               f"   total {dec[ran].sum(1).mean():8.0f} cycles/block", flush=True)
         print(f"  decode fast path (entered at sF, one segment): {b[ran, 15].mean():.3f} of the blocks decoded",
