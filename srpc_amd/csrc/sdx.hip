@@ -88,6 +88,8 @@ constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
 constexpr uint32_t kEnt = kWin + 1 + kX;         // table entries per block: the window's, the extra slot,
                                                  // then the landing slots
 constexpr uint32_t kHdr = 8;                     // header words per block
+constexpr uint32_t kRepairMin = 16;              // segments past which k_sx_spec repairs its chunks
+constexpr uint32_t kRepairMax = 16;              // repair passes at most
 constexpr uint32_t kGroup = 64;                  // blocks per group of the scan (a lane per block)
 constexpr int kMaxNC = 3;                        // chars values carried per state (string fields 0..ns-2)
 constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block (each >= 8 bytes)
@@ -101,7 +103,7 @@ constexpr int kKeep = 4;                         // table entries per block the 
 constexpr uint64_t kCnt40 = (1ull << 40) - 1;
 constexpr uint32_t kNoPrim = 0xFF;
 constexpr uint32_t kListCap = 4;                 // record starts a 32-byte chunk holds (records >= 8 bytes apart)
-static_assert(kSB / 32 == kBlock && kListCap == 4, "a lane per landing-bitmap word, over its own list entries");
+static_assert(kSB / 32 == kBlock && kListCap == 4, "a wave's part of the chunk lists holds 128 u16 landing slots");
 constexpr uint32_t kDead = 0x81;                 // stop bits of a group-table chain given up (k_sx_groups)
 
 // control words (scratch; k_sx_spec block 0 zeroes them each call)
@@ -572,6 +574,14 @@ __device__ __forceinline__ uint32_t next_bit(const uint64_t* m, uint32_t i) {
     uint64_t v = m[w] & (~0ull << (i & 63));
     while (!v && ++w < 4) v = m[w];
     return w < 4 ? 64 * w + __builtin_ctzll(v) : 256;
+}
+
+// Last set bit at index <= i of a 256-bit mask (4 words in LDS), or 256.
+__device__ __forceinline__ uint32_t prev_bit(const uint64_t* m, uint32_t i) {
+    int w = static_cast<int>(i >> 6);
+    uint64_t v = m[w] & ((i & 63) == 63 ? ~0ull : ((2ull << (i & 63)) - 1));
+    while (!v && --w >= 0) v = m[w];
+    return w >= 0 ? 64 * w + 63 - __builtin_clzll(v) : 256;
 }
 
 // A block's chunks in LDS (both the speculation and the decode keep them):
@@ -1203,6 +1213,59 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
     __syncthreads();
     SXP(1);
     link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
+    // Repair, in blocks the speculation cut into many segments (zero-heavy
+    // bytes, where most positions parse): each chunk whose predecessor's walk
+    // exits inside it walks again from that exit (or has no start when the
+    // exit is past it), all at once, until nothing changes or kRepairMax
+    // passes.  A run of k wrong chunks after a right one is right after k
+    // passes; the chains then cross the block in a few segment jumps instead
+    // of record by record (here and in k_sx_decode, which walks its chunks
+    // from the repaired starts).  A first pass that joins fewer than 4
+    // segments ends the repair.  Random blocks have 1-4 segments: not taken.
+    {
+        uint32_t ntail = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ntail += __builtin_popcountll(C.tail[k]);
+#ifdef SRPC_SX_NOREPAIR
+        if (false) {  // (A/B)
+#else
+        if (__builtin_expect(ntail > kRepairMin && !(a.mode & 3), 0)) {
+#endif
+#pragma nounroll
+            for (uint32_t pass = 0; pass < kRepairMax; ++pass) {
+                const uint32_t pc = tid ? prev_bit(C.has, tid - 1) : 256;
+                uint64_t nsp = sp;
+                if (pc < 256 && !C.stop[pc] && clo < b1) {
+                    const uint64_t e = C.exit[pc];
+                    if (e >= chi) nsp = ~0ull;
+                    else if (e >= clo) nsp = e;
+                }
+                const bool redo = nsp != sp;
+                if (!__syncthreads_or(redo)) break;  // (every chunk read its predecessor's exit)
+                if (redo) {
+                    sp = nsp;
+#pragma unroll
+                    for (int k = 0; k <= kMaxNC; ++k) cch[k] = 0;
+                    walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, L.list + tid * kListCap);
+                    C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
+                    C.exit[tid] = cexit;
+                    C.stop[tid] = static_cast<uint8_t>(cstop);
+                }
+                const uint64_t hm2 = __ballot(sp != ~0ull);
+                if (lane == 0) C.has[tid >> 6] = hm2;
+                __syncthreads();
+                link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
+                // a first pass that joins few segments (long runs of wrong
+                // chunks, e.g. zero bytes read in the wrong alignment: one
+                // chunk a pass) is not repeated
+                uint32_t nt = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nt += __builtin_popcountll(C.tail[k]);
+                if (pass == 0 && nt + 4 > ntail) break;
+            }
+            if (clo < b1) S.spec[b * kBlock + tid] = sp == ~0ull ? kNoSpec : static_cast<uint8_t>(sp - clo);
+        }
+    }
     // the chunks' records in order (the block's whole record list when its
     // chunks form one segment: k_sx_decode's fast path takes it from here)
     {
