@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
             uint32_t pj = ~0u;
             const bool zf = W < (1ull << 32) && !(a.mode & 4);
             uint64_t mask = zf ? chunk_mask_z(a, L.st, at, clo, chi, &pj) : chunk_mask(a, L.st, at, clo, chi);
-            const uint64_t passing = mask;
+            bool tried = false;  // the first cluster's pick was tested
             // the first cluster of passing positions (8 bytes from the first):
             // its smallest first string length is the true start (a start
             // 1-3 bytes early reads the true length shifted up), tested first
@@ -1143,6 +1143,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
                 }
                 uint32_t err = SRPC_STATUS_BOUNDS;
                 uint64_t tmp[kMaxNC + 1] = {};
+                tried = pick != ~0ull;
                 const uint64_t q1 = pick != ~0ull ? parse_rd<NC>(a, so, pick, &err, tmp) : 0;
                 bool ok = !err;
                 if (ok && a.plaus > 1 && q1 != W) {
@@ -1157,9 +1158,48 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
                     for (int k = 0; k < NC; ++k) sch1[k] = tmp[k];
                 }
             }
-            if (sp == ~0ull) {
-                // otherwise: the first plausible position, then of the
-                // plausible ones within 8 bytes the smallest first length
+            SXP_ADD(4, sp == ~0ull && mask ? 1 : 0);
+            if (sp == ~0ull && __builtin_popcountll(mask) <= 16) {
+                // otherwise, in a chunk where few positions pass: cluster by
+                // cluster (8 bytes from a cluster's first passing position),
+                // its smallest first length tested for plausibility (the first
+                // cluster's was, above).  A chunk of a schema whose later
+                // string lengths also have zero high bytes (zh4: int8, string,
+                // int16, string) often starts with such a false cluster:
+                // testing every position in order cost zh4 random ~130
+                // fallbacks x ~8 plausibility tests a block (34 % of its
+                // throughput, profiles/r05_sdx_ab.log).  (A start missed here
+                // is only a slower chain, never a wrong one.)
+                uint64_t m = mask;
+                bool skip = tried;
+                while (m) {
+                    const uint32_t j0 = __builtin_ctzll(m);
+                    uint64_t cl = (m >> j0) & 0xff;
+                    m &= j0 + 8 < 64 ? ~0ull << (j0 + 8) : 0ull;
+                    if (skip) {
+                        skip = false;
+                        continue;
+                    }
+                    uint64_t best = ~0ull, pk = clo + j0;
+                    while (cl) {
+                        const uint64_t q = clo + j0 + __builtin_ctzll(cl);
+                        cl &= cl - 1;
+                        const uint64_t l = so.u64(q + a.first_len_at);
+                        if (l < best) {
+                            best = l;
+                            pk = q;
+                        }
+                    }
+                    if (plausible(a, so, pk)) {
+                        sp = pk;
+                        break;
+                    }
+                }
+            } else if (sp == ~0ull) {
+                // where most positions pass (zero-heavy bytes): the first
+                // plausible position, then of the plausible ones within 8
+                // bytes the smallest first length
+                const uint64_t passing = mask;
                 while (mask) {
                     const uint32_t j = __builtin_ctzll(mask);
                     if (plausible(a, so, clo + j)) {
