@@ -684,14 +684,10 @@ struct WaveRd {
 };
 constexpr uint32_t kWaveStage = kSB + kMargin + 32;  // one block + margin, 16-byte aligned either side
 
-// The cursor's way through a block from x when x is in none of its table's
-// slots (a miss): the whole wave copies the block into its LDS stage (16-byte
-// loads, all in flight at once), then every lane that missed walks record by
-// record from there.  Called by every lane of the wave (uniform); lanes with
-// !mine get nothing.
-template <int NC>
-__device__ St<NC> walk_miss(const SxArgs& a, const uint8_t* w, uint8_t* stage, uint64_t b0, uint64_t b1, uint64_t x,
-                            bool mine) {
+// A wave's copy of block [b0, min(b1 + kMargin, W)) into its LDS stage
+// (16-byte loads, all in flight at once); every lane of the wave takes part.
+__device__ __forceinline__ WaveRd stage_wave(const SxArgs& a, const uint8_t* w, uint8_t* stage, uint64_t b0,
+                                             uint64_t b1) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t hi = min<uint64_t>(b1 + kMargin, a.W);
     const uint64_t A = (reinterpret_cast<uint64_t>(w) + b0) & ~15ull;
@@ -709,22 +705,7 @@ __device__ St<NC> walk_miss(const SxArgs& a, const uint8_t* w, uint8_t* stage, u
         if (gi < ng) *reinterpret_cast<u32x4*>(stage + 16 * gi) = v[k];
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the wave's LDS writes before its reads
-    St<NC> g{};
-    if (!mine) return g;
-    const WaveRd rd{(global_u8*)w, (lds_u8c*)stage, A - reinterpret_cast<uint64_t>(w), b0, hi, a.prefix};
-    uint64_t q = x;
-    while (q < b1) {
-        uint32_t err;
-        const uint64_t q2 = parse_rd<NC>(a, rd, q, &err, g.ch);
-        if (err) {
-            g.stop = 1 | (err << 1);
-            break;
-        }
-        ++g.cnt;
-        q = q2;
-    }
-    g.x = q;
-    return g;
+    return WaveRd{(global_u8*)w, (lds_u8c*)stage, A - reinterpret_cast<uint64_t>(w), b0, hi, a.prefix};
 }
 
 template <int NC>
@@ -842,8 +823,8 @@ __device__ __forceinline__ StagedRd stage_block(const SxArgs& a, const uint8_t* 
 
 // Chunk tid's records from its start sp (or none): count, the position after
 // them, chars, stop bits, their starts (up to cap, offsets in the chunk).
-template <int NC>
-__device__ __forceinline__ void walk_chunk(const SxArgs& a, const StagedRd& rd, uint64_t sp, uint64_t chi,
+template <int NC, class Rd>
+__device__ __forceinline__ void walk_chunk(const SxArgs& a, const Rd& rd, uint64_t sp, uint64_t chi,
                                            uint32_t* cnt, uint64_t* exit, uint64_t (&ch)[kMaxNC + 1], uint32_t* stop,
                                            uint8_t* list) {
     *cnt = 0;
@@ -894,6 +875,105 @@ __device__ __forceinline__ void link_chunks(Chunks<NC>& L, uint64_t b0, uint64_t
         }
     }
     __syncthreads();
+}
+
+// The cursor's way through a block from x when x is in none of its table's
+// slots (a miss), by one wave (every lane calls it; lanes with !mine get
+// nothing): the block is staged in the wave's LDS, its 256 chunks are walked
+// again from phase 1's speculated starts -- four a lane, as k_sx_decode walks
+// them -- and linked into segments (wave scans), then each missing lane's
+// chain crosses the block in segment jumps, parsing records only where it is
+// off the speculation.  A record-by-record walk of a block by one lane cost
+// ~250 ns a record (8 KiB of 19-byte records: ~0.1 ms, serial in k_sx_top).
+template <int NC>
+__device__ St<NC> walk_miss(const SxArgs& a, const uint8_t* w, const SxScratch& S, uint64_t blk, uint8_t* stage,
+                            Chunks<NC>& C, uint64_t b0, uint64_t b1, uint64_t x, bool mine) {
+    const uint32_t lane = threadIdx.x & 63;
+    const WaveRd rd = stage_wave(a, w, stage, b0, b1);
+    if (lane < 4) {
+        C.has[lane] = 0;
+        C.tail[lane] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t c = 4 * lane + q;
+        const uint64_t clo = b0 + static_cast<uint64_t>(c) * kSC, chi = min<uint64_t>(clo + kSC, b1);
+        const uint8_t sb = clo < b1 ? S.spec[blk * kBlock + c] : kNoSpec;
+        const uint64_t sp = sb == kNoSpec ? ~0ull : clo + sb;
+        uint64_t ch[kMaxNC + 1] = {};
+        uint32_t cnt, cstop;
+        uint64_t cexit;
+        walk_chunk<NC>(a, rd, sp, chi, &cnt, &cexit, ch, &cstop, nullptr);
+        C.start[c] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
+        C.exit[c] = cexit;
+        C.stop[c] = static_cast<uint8_t>(cstop);
+        C.pcnt[c] = cnt;
+        if constexpr (NC > 0) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) C.pch[k][c] = ch[k];
+        }
+        if (sp != ~0ull) atomicOr(reinterpret_cast<unsigned long long*>(&C.has[c >> 6]), 1ull << (c & 63));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // segment tails (as link_chunks), then exclusive scans of the records and
+    // chars over the chunks: a lane's four in order, the lanes by a wave scan
+    uint64_t tot = 0, totc[kMaxNC + 1] = {};
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t c = 4 * lane + q;
+        if (C.start[c] != kNoStart) {
+            const uint32_t nxt = next_bit(C.has, c + 1);
+            if (C.stop[c] || nxt >= kBlock || C.exit[c] != b0 + C.start[nxt])
+                atomicOr(reinterpret_cast<unsigned long long*>(&C.tail[c >> 6]), 1ull << (c & 63));
+        }
+        tot += C.pcnt[c];
+        if constexpr (NC > 0) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) totc[k] += C.pch[k][c];
+        }
+    }
+    uint64_t inc = tot, incc[kMaxNC + 1];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) incc[k] = totc[k];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= static_cast<uint32_t>(d)) inc += y;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            const uint64_t z = __shfl_up(incc[k], d, 64);
+            if (lane >= static_cast<uint32_t>(d)) incc[k] += z;
+        }
+    }
+    uint64_t run = inc - tot, runc[kMaxNC + 1];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) runc[k] = incc[k] - totc[k];
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t c = 4 * lane + q;
+        const uint32_t v = C.pcnt[c];
+        C.pcnt[c] = static_cast<uint32_t>(run);
+        run += v;
+        if constexpr (NC > 0) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const uint64_t y = C.pch[k][c];
+                C.pch[k][c] = runc[k];
+                runc[k] += y;
+            }
+        }
+    }
+    if (lane == 63) {
+        C.pcnt[kBlock] = static_cast<uint32_t>(run);
+        if constexpr (NC > 0) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) C.pch[k][kBlock] = runc[k];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (!mine) return St<NC>{};
+    return walk_chain<NC, false>(a, rd, C, b0, b1, x, nullptr, nullptr);
 }
 
 // Workgroup i -> block.  Dispatch order by default; with SRPC_SX_XCD the
@@ -1483,7 +1563,8 @@ struct Held {
 template <int NC>
 __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w, const SxScratch& S,
                                               const Held<NC>& hv, uint32_t l, uint64_t blk, St<NC>& s, bool* miss,
-                                              bool* off, uint8_t* stage, uint16_t* xs, bool may_walk = true) {
+                                              bool* off, uint8_t* stage, Chunks<NC>* mc, uint16_t* xs,
+                                              bool may_walk = true) {
     // the held words of lane l (uniform reads, every lane takes part)
     const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l), h3 = rl64(hv.h3, l), h4 = rl64(hv.h4, l);
     const uint32_t meta = __builtin_amdgcn_readlane(hv.meta, l);
@@ -1501,7 +1582,7 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
     const bool walk = act && sl.idx < 0 && may_walk;
     // every lane of the wave takes part in the staging of walk_miss
     St<NC> mw{};
-    if (__ballot(walk)) mw = walk_miss<NC>(a, w, stage, b0, b1, s.x, walk);
+    if (__ballot(walk)) mw = walk_miss<NC>(a, w, S, blk, stage, *mc, b0, b1, s.x, walk);
     if (act && sl.idx < 0 && !may_walk) {  // a chain the caller gives up on instead of walking it
         s.stop = kDead;
         return;
@@ -1554,6 +1635,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     __shared__ uint16_t xss[kBlock / 64][kXA];
     uint8_t* stage = stages[threadIdx.x >> 6];
+    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
     uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     uint64_t* q = S.gp + g * (kHdr + ew<NC>());
@@ -1574,7 +1656,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
             const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
             if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
             St<NC> t = s;
-            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, xs, primary);
+            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs, primary);
             if (act) s = t;
         }
         if (act) st_store<NC>(S.gent + (g * kEnt + idx) * ew<NC>(), s);
@@ -1604,6 +1686,7 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
     const uint32_t lane = threadIdx.x;
     const uint64_t W = a.W;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
+    __shared__ Chunks<NC> mch;  // walk_miss's chunks
     __shared__ uint16_t xs[kXA];
     St<NC> s{};
     bool miss = false, off = false;
@@ -1721,7 +1804,7 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
                     t.cnt -= sl.sub;
                     st_add<NC>(s, t);
                 } else {
-                    st_add<NC>(s, walk_miss<NC>(a, w, stage, b0, b1, s.x, true));
+                    st_add<NC>(s, walk_miss<NC>(a, w, S, j, stage, mch, b0, b1, s.x, true));
                     miss = true;
                 }
             }
@@ -1787,6 +1870,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     __shared__ uint16_t xss[kBlock / 64][kXA];
     uint8_t* stage = stages[threadIdx.x >> 6];
+    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
     uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     for (uint32_t j = 0; j < nbk;) {
@@ -1817,7 +1901,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
         st_store<NC>(v, s);
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) out[k] = lane == j ? v[k] : out[k];
-        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage, xs);
+        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs);
         ++j;
     }
     if (lane < nbk)
