@@ -1349,7 +1349,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
 #ifdef SRPC_SX_NOREPAIR
         if (false) {  // (A/B)
 #else
-        if (__builtin_expect(ntail > kRepairMin && !(a.mode & 3), 0)) {
+        if (__builtin_expect(ntail > kRepairMin, 0)) {
 #endif
 #pragma nounroll
             for (uint32_t pass = 0; pass < kRepairMax; ++pass) {
@@ -1374,15 +1374,22 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
                 const uint64_t hm2 = __ballot(sp != ~0ull);
                 if (lane == 0) C.has[tid >> 6] = hm2;
                 __syncthreads();
-                link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
-                // a first pass that joins few segments (long runs of wrong
-                // chunks, e.g. zero bytes read in the wrong alignment: one
-                // chunk a pass) is not repeated
-                uint32_t nt = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) nt += __builtin_popcountll(C.tail[k]);
-                if (pass == 0 && nt + 4 > ntail) break;
+                // (the passes need only the starts, exits and stops: the
+                // segments' scans are built once, after the last pass)
+                if (pass == 0) {
+                    // a first pass that joins few segments (long runs of
+                    // wrong chunks, e.g. zero bytes read in the wrong
+                    // alignment: one chunk a pass) is not repeated
+                    bool tail = false;
+                    if (sp != ~0ull) {
+                        const uint32_t nxt = next_bit(C.has, tid + 1);
+                        tail = cstop || nxt >= kBlock || cexit != b0 + C.start[nxt];
+                    }
+                    const uint32_t nt = static_cast<uint32_t>(__syncthreads_count(tail));
+                    if (nt + 4 > ntail) break;
+                }
             }
+            link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);
             if (clo < b1) S.spec[b * kBlock + tid] = sp == ~0ull ? kNoSpec : static_cast<uint8_t>(sp - clo);
         }
     }
