@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 
-TOOLS = {"e2e_square": "e2e_square.hip", "aos_bench": "aos_bench.hip"}
+TOOLS = {"e2e_square": "e2e_square.hip", "aos_bench": "aos_bench.hip",
+         "capture_ring": "capture_ring.hip"}  # (plain HIP: the library is linked, not used)
 
 
 def build(name: str = "e2e_square") -> str:
@@ -31,4 +32,4 @@ def build(name: str = "e2e_square") -> str:
 
 
 if __name__ == "__main__":
-    print(build())
+    print(build(sys.argv[1] if len(sys.argv) > 1 else "e2e_square"))
