@@ -65,11 +65,11 @@ constexpr uint32_t kMargin = 1536;               // staged bytes past the block
 // record that starts in the kPre bytes before the block (its premargin) and
 // ends in the block past the window -- the true entry of a record that
 // straddles the block's start by up to kPre bytes, whatever the speculation
-// made of the block.  Wave 0 finds them alone, from the premargin staged
-// with the block, while waves 1-3 have left (no barrier,
-// nothing read from global memory; a first version that scanned with the
-// whole workgroup cost every random row 25-30 %, one that read the premargin
-// from global memory 10-23 %: profiles/r05_sdx_ab.log).  A/B build
+// made of the block.  Wave 1 finds them alone (land_slots), from the
+// premargin staged with the block, while wave 0 builds the window table (no
+// barrier, nothing read from global memory; a whole-workgroup scan with
+// barriers cost every random row 25-30 %, a wave-0 scan after the table
+// 10-28 %, this one 2-9 %: profiles/r05_sdx_ab.log).  A/B build
 // SRPC_SX_NOLAND leaves them out.
 #ifndef SRPC_SX_NOLAND
 constexpr uint32_t kPre = 1024;                  // premargin: bytes before the block scanned for landings
@@ -999,7 +999,7 @@ struct SpecLds {
     // per chunk: its records' starts (offsets in the chunk); then wave 0's
     // part (the record list written out) holds the landing slots
     alignas(4) uint8_t list[kBlock * kListCap];
-    uint32_t s_nx;  // landings found (wave 0's counter)
+    uint32_t s_nx;  // landings found (wave 1's counter)
 };
 static_assert(64 * kListCap >= 2 * kX, "the landing slots fit wave 0's part of the chunk lists");
 
