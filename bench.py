@@ -39,7 +39,9 @@ ALG_BYTES_PER_REC = 32          # per kernel: pack reads 4x4 B + writes 16 B; un
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE, else 1); without torchrun N > 1 spawns "
+                         "N rank processes itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--records", type=int, default=1 << 24, help="records per GPU")
@@ -57,6 +59,94 @@ def parse():
                     help="strong-scaling line beside the weak one: this many records in all, "
                          "split over the ranks (configs[3]: 64M); 0 disables")
     return ap.parse_args()
+
+
+XGMI_LINK_GBPS = 153.0  # per xGMI link and direction (the task's MI355X figure: 7 links x ~153 GB/s)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_plan(gpus, env: dict, device_count: int, backend: str) -> dict:
+    """What `bench.py --gpus N` does, decided without touching a GPU.
+
+    - Under a launcher (WORLD_SIZE set, as torch.distributed.run does): run as
+      that rank; --gpus, when given, must equal WORLD_SIZE.
+    - No launcher and N > 1: spawn N rank processes (children of this one,
+      never an exec) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank
+      r on device r; rank 0 prints the line.
+    - N = 1: run in this process.
+    With the NCCL backend every rank needs its own GPU: fewer visible devices
+    than ranks is an error (gloo may share one GPU: a rehearsal only).
+    Returns {"mode": "rank"|"spawn"|"single", "world": N, "envs": [...]} or
+    {"error": message}."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        try:
+            world = int(ws)
+        except ValueError:
+            return {"error": f"WORLD_SIZE={ws!r} is not an integer"}
+        if world < 1:
+            return {"error": f"WORLD_SIZE={world}"}
+        if gpus is not None and gpus != world:
+            return {"error": f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"}
+        mode = "rank" if world > 1 else "single"
+    else:
+        world = 1 if gpus is None else gpus
+        if world < 1:
+            return {"error": f"--gpus {world}: need at least one GPU"}
+        mode = "spawn" if world > 1 else "single"
+    if world > 1 and backend == "nccl" and device_count < world:
+        return {"error": f"{world} ranks over RCCL need {world} GPUs, {device_count} visible "
+                         f"(one rank per GPU; --dist-backend gloo rehearses N > 1 on fewer)"}
+    if world == 1 and device_count < 1:
+        return {"error": "no GPU visible"}
+    out = {"mode": mode, "world": world, "envs": []}
+    if mode == "spawn":
+        port = env.get("MASTER_PORT") or str(free_port())
+        for r in range(world):
+            e = dict(env)
+            e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                     GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            out["envs"].append(e)
+    return out
+
+
+def spawn_ranks(envs: list, argv: list) -> int:
+    """Runs one child per rank (this script, same arguments) and waits; when
+    one fails the others are stopped (their PIDs only) and its code returned."""
+    import signal
+    import subprocess
+
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e) for e in envs]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        print(f"bench.py: a rank failed with exit code {rc}; stopped the others", file=sys.stderr, flush=True)
+    return rc
 
 
 def committed_profiles(dom_name: str, n: int) -> dict:
@@ -421,9 +511,18 @@ def cpu_baseline(n: int, target_s: float) -> dict | None:
 def main() -> None:
     args = parse()
     import torch
+
+    # torch.cuda.device_count() does not initialise the GPU on this image: the
+    # plan is made, and ranks spawned, before any HIP call in this process
+    plan = launch_plan(args.gpus, dict(os.environ), torch.cuda.device_count(), args.dist_backend)
+    if "error" in plan:
+        print(f"bench.py: {plan['error']}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan["mode"] == "spawn":
+        sys.exit(spawn_ranks(plan["envs"], sys.argv[1:]))
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = plan["world"]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())
@@ -585,8 +684,14 @@ def main() -> None:
         dist.barrier()
         g_ms = (time.perf_counter() - g0) * 1e3 / reps
         moved = n * (world - 1) * REC_BYTES
+        # every sender has its own link into the root: the floor is one shard
+        # over one link, (G - 1) links in parallel
+        floor_ms = n * REC_BYTES / (XGMI_LINK_GBPS * 1e9) * 1e3
         gather = {"ms": round(g_ms, 3), "bytes_to_root": moved,
                   "root_ingress_GBps": round(moved / g_ms / 1e6, 1),
+                  "expected_ms_at_link_peak": round(floor_ms, 3),
+                  "expected_root_ingress_GBps": round((world - 1) * XGMI_LINK_GBPS, 1),
+                  "frac_of_link_floor": round(floor_ms / g_ms, 3),
                   "collective": ("libsrpc_gpu srpc_gather_wire: RCCL ncclSend/ncclRecv to rank 0 in one group"
                                  if comm is not None else
                                  "torch.distributed RCCL gather" if args.dist_backend == "nccl"

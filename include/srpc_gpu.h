@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SRPC_GPU_ABI_VERSION 7
+#define SRPC_GPU_ABI_VERSION 8
 
 /* Field kinds = the IDL type table of the reference (parser.hpp:253-290).
  * Nested message fields are flattened into their members by the caller. */
@@ -322,6 +322,27 @@ int srpc_comm_rank(const srpc_comm* comm, int* rank, int* nranks);
 /* Each rank contributes one u64 (e.g. its shard's wire bytes, read from the
  * last entry of its d_rec_offs for string schemas); d_out gets nranks. */
 int srpc_allgather_u64(srpc_comm* comm, const uint64_t* d_in, uint64_t* d_out, void* stream);
+
+/* The gather's plan, host arithmetic only: the operations rank `rank` of
+ * srpc_gather_wire enqueues, in order -- a non-root rank one SEND of its shard
+ * (none when it is empty); the root a RECV from every other rank with bytes
+ * and a COPY of its own shard, each at byte offset sum(h_all_bytes[0..peer))
+ * of the root's wire.  The same argument checks as srpc_gather_wire
+ * (SRPC_E_INVALID, SRPC_E_CAPACITY) in the same order; ops gets at most
+ * cap_ops entries (SRPC_E_CAPACITY when nranks would not fit), *nops the
+ * count.  srpc_gather_wire runs exactly this list, so a transport other
+ * than RCCL (a test's gloo) can replay it byte for byte. */
+#define SRPC_GATHER_SEND 1
+#define SRPC_GATHER_RECV 2
+#define SRPC_GATHER_COPY 3
+typedef struct srpc_gather_op {
+    int32_t kind;    /* SRPC_GATHER_SEND / _RECV / _COPY                       */
+    int32_t peer;    /* SEND: the root; RECV: the sender; COPY: the root itself */
+    uint64_t offset; /* byte offset into the root's wire (0 for SEND)           */
+    uint64_t bytes;
+} srpc_gather_op;
+int srpc_gather_plan(int rank, int nranks, int root, uint64_t shard_bytes, const uint64_t* h_all_bytes,
+                     uint64_t root_cap, srpc_gather_op* ops, int cap_ops, int* nops);
 
 /* Gather: every rank calls it with its shard's wire bytes; the root receives
  * shard r at byte offset sum(h_all_bytes[0..r)) of d_root_wire (root_cap

@@ -67,6 +67,7 @@ SIGNATURES = {
     "srpc_comm_destroy": (C.c_int, [_vp]),
     "srpc_comm_rank": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "srpc_allgather_u64": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "srpc_gather_plan": (C.c_int, [C.c_int, C.c_int, C.c_int, _u64, _vp, _u64, _vp, C.c_int, C.POINTER(C.c_int)]),
     "srpc_gather_wire": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp, C.c_int, _vp]),
     "srpc_group_gather_wire": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _u64, C.c_int, _vp]),
     "srpc_group_pack_gather": (C.c_int, [_vp, _vp, C.c_int, _vp, _u64, _vp, _vp, _u64, C.c_int, _vp]),
@@ -89,6 +90,15 @@ SIGNATURES = {
 class SchemaDesc(C.Structure):
     _fields_ = [("nfields", C.c_uint32), ("kinds", C.POINTER(_i32)),
                 ("prefix", C.POINTER(C.c_uint8)), ("prefix_len", C.c_uint32)]
+
+
+class GatherOp(C.Structure):
+    _fields_ = [("kind", _i32), ("peer", _i32), ("offset", _u64), ("bytes", _u64)]
+
+
+SRPC_GATHER_SEND = 1
+SRPC_GATHER_RECV = 2
+SRPC_GATHER_COPY = 3
 
 
 class UnpackStatus(C.Structure):

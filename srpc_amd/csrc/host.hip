@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstdint>
 #include <map>
@@ -40,17 +41,23 @@ struct Pipe {
     hipStream_t in = nullptr, k = nullptr, out = nullptr;
     hipEvent_t start = nullptr;
     hipEvent_t fence[3] = {};    // an error's drain: the last work of each internal stream
+    hipEvent_t idle[3] = {};     // recorded on return to the pool: the pipe's streams are idle once all three fired
+    hipStream_t caller = nullptr;  // the caller stream of the call that last used it
     std::vector<hipEvent_t> ev;  // 3 per ring slot: input copied, kernel done, output copied
 };
 
-// Pipes are pooled per device: a call borrows one -- any
-// free pipe, or a new one when every pipe is lent to a call in another thread
-// -- and returns it when its work is enqueued.  The pool grows to the number
-// of calls ever in flight at once, not with the threads that made them, and a
-// thread that exits leaks nothing.  Pipes live for the process (destroying
-// streams while HIP tears down at exit is not safe).  Calls from one thread on
-// different caller streams share a pipe, so their copies queue in call order
-// on its streams -- the same order the calls were made in.
+// Pipes are pooled per device: a call borrows one and returns
+// it once its work is ENQUEUED, but a returned pipe may still be moving that
+// call's bytes for milliseconds.  So a call takes, in order:
+// a free pipe last used with its own caller stream (its work is ordered
+// behind that stream's earlier calls anyway: nothing is serialised that was
+// not already), else a free pipe whose streams are idle (its `idle` events
+// have fired), else a new pipe.  Calls on different caller streams therefore
+// never queue their copies behind each other on shared internal streams while
+// the other's are in flight; the pool grows to the number of calls in flight
+// at once, not with the threads that made them, and a thread that exits
+// leaks nothing.  Pipes live for the process (destroying streams while HIP
+// tears down at exit is not safe).
 struct PipePool {
     std::mutex mu;
     std::map<int, std::vector<Pipe*>> free;
@@ -68,28 +75,50 @@ Pipe* make_pipe() {
               hipStreamCreateWithFlags(&p->out, fl) == hipSuccess &&
               hipEventCreateWithFlags(&p->start, hipEventDisableTiming) == hipSuccess;
     for (auto& e : p->fence) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    for (auto& e : p->idle) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (ok) return p;
     for (hipStream_t q : {p->in, p->k, p->out})
         if (q) (void)hipStreamDestroy(q);
-    for (hipEvent_t e : {p->start, p->fence[0], p->fence[1], p->fence[2]})
+    for (hipEvent_t e : {p->start, p->fence[0], p->fence[1], p->fence[2], p->idle[0], p->idle[1], p->idle[2]})
         if (e) (void)hipEventDestroy(e);
     delete p;
     (void)hipGetLastError();
     return nullptr;
 }
 
-// A pipe of `device` (the current device) with a ring of `depth`, returned by
-// ~Lease.
+// True when every piece of work last enqueued on the pipe's streams has run
+// (an event never recorded counts as fired).  A not-ready query leaves no
+// error behind for the call's final hipGetLastError.
+bool pipe_idle(Pipe* p) {
+    for (hipEvent_t e : p->idle) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) continue;
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
+thread_local const Pipe* t_last_pipe = nullptr;  // test hook: the pipe this thread's last call used
+
+// A pipe of `device` (the current device) with a ring of `depth` for a call
+// on `caller`, returned by ~Lease (see the pool's comment for the choice).
 struct Lease {
     int device;
+    hipStream_t caller;
     Pipe* p = nullptr;
-    Lease(int dev, uint32_t depth) : device(dev) {
+    Lease(int dev, uint32_t depth, hipStream_t s) : device(dev), caller(s) {
         {
             std::lock_guard<std::mutex> lk(pool().mu);
             auto& v = pool().free[dev];
-            if (!v.empty()) {
-                p = v.back();
-                v.pop_back();
+            size_t pick = v.size();
+            for (size_t i = 0; i < v.size() && pick == v.size(); ++i)
+                if (v[i]->caller == s) pick = i;
+            for (size_t i = 0; i < v.size() && pick == v.size(); ++i)
+                if (pipe_idle(v[i])) pick = i;
+            if (pick < v.size()) {
+                p = v[pick];
+                v.erase(v.begin() + static_cast<std::ptrdiff_t>(pick));
             }
         }
         if (!p) {
@@ -98,6 +127,7 @@ struct Lease {
             std::lock_guard<std::mutex> lk(pool().mu);
             ++pool().made[dev];
         }
+        t_last_pipe = p;
         while (p->ev.size() < 3ull * depth) {
             hipEvent_t e;
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
@@ -109,6 +139,10 @@ struct Lease {
     }
     void release() {
         if (!p) return;
+        // the last work of each internal stream: the pipe is idle once these fire
+        hipStream_t q[3] = {p->in, p->k, p->out};
+        for (int i = 0; i < 3; ++i) (void)hipEventRecord(p->idle[i], q[i]);
+        p->caller = caller;
         std::lock_guard<std::mutex> lk(pool().mu);
         pool().free[device].push_back(p);
         p = nullptr;
@@ -189,13 +223,12 @@ bool two_streams() {
     return e && e[0] == '2';
 }
 
-// Test hook (SRPC_HOST_FAIL_AT=k, read per call): the chunked ring fails at
-// chunk k as a HIP error would, after chunks 0..k-1 are enqueued -- the
-// error path's drain is tested with copies really in flight.
-uint64_t fail_at() {
-    const char* e = std::getenv("SRPC_HOST_FAIL_AT");
-    return e && *e ? std::strtoull(e, nullptr, 10) : UINT64_MAX;
-}
+// Test hook (srpc_debug_host_fail_at(k), not in include/; off unless a test
+// arms it): the chunked ring fails at chunk k as a HIP error would, after
+// chunks 0..k-1 are enqueued -- the error path's drain is tested with copies
+// really in flight.  Nothing in the environment can make a real call fail.
+std::atomic<uint64_t> g_fail_at{UINT64_MAX};
+uint64_t fail_at() { return g_fail_at.load(std::memory_order_relaxed); }
 
 int check_pipe_args(const srpc_plan* p, uint64_t chunk, uint32_t depth) {
     if (!p) return SRPC_E_INVALID;
@@ -289,7 +322,7 @@ int srpc_gpu_pack_host(const srpc_plan* p, const void* const* h_cols, uint64_t n
     if (reinterpret_cast<uintptr_t>(d_scratch) % kAlignScratch) return SRPC_E_ALIGN;
     auto s = static_cast<hipStream_t>(stream);
     if (capturing(s)) return SRPC_E_UNSUPPORTED;
-    Lease lease(p->device, depth);
+    Lease lease(p->device, depth, s);
     Pipe* P = lease.p;
     if (!P) return SRPC_E_HIP;
     const bool two = two_streams();
@@ -385,7 +418,7 @@ int srpc_gpu_unpack_host(const srpc_plan* p, const uint8_t* h_wire, uint64_t wir
         }
         return ret;
     }
-    Lease lease(p->device, depth);
+    Lease lease(p->device, depth, s);
     Pipe* P = lease.p;
     if (!P) return SRPC_E_HIP;
     const bool two = two_streams();
@@ -450,4 +483,14 @@ extern "C" __attribute__((visibility("default"))) uint64_t srpc_debug_host_pipes
     std::lock_guard<std::mutex> lk(pool().mu);
     auto it = pool().made.find(device);
     return it == pool().made.end() ? 0 : it->second;
+}
+
+// Test hooks (not in include/): arm the chunked ring's injected failure at
+// chunk k (UINT64_MAX disarms), and the pipe this thread's last chunked call
+// borrowed (an opaque id: which calls shared a pipe).
+extern "C" __attribute__((visibility("default"))) void srpc_debug_host_fail_at(uint64_t k) {
+    g_fail_at.store(k, std::memory_order_relaxed);
+}
+extern "C" __attribute__((visibility("default"))) uint64_t srpc_debug_host_last_pipe(void) {
+    return reinterpret_cast<uintptr_t>(t_last_pipe);
 }

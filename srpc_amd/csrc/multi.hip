@@ -145,40 +145,68 @@ int srpc_allgather_u64(srpc_comm* c, const uint64_t* d_in, uint64_t* d_out, void
     return nccl_rc(ncclAllGather(d_in, d_out, 1, ncclUint64, c->comm, static_cast<hipStream_t>(stream)));
 }
 
+int srpc_gather_plan(int rank, int nranks, int root, uint64_t shard_bytes, const uint64_t* h_all_bytes,
+                     uint64_t root_cap, srpc_gather_op* ops, int cap_ops, int* nops) {
+    if (nranks <= 0 || rank < 0 || rank >= nranks || root < 0 || root >= nranks || !nops) return SRPC_E_INVALID;
+    *nops = 0;
+    if (cap_ops > 0 && !ops) return SRPC_E_INVALID;
+    if (rank != root) {
+        if (!shard_bytes) return SRPC_OK;
+        if (cap_ops < 1) return SRPC_E_CAPACITY;
+        ops[0] = srpc_gather_op{SRPC_GATHER_SEND, root, 0, shard_bytes};
+        *nops = 1;
+        return SRPC_OK;
+    }
+    // the root: sizes summed without overflow, its own entry its shard, the
+    // concatenation within its buffer -- all before any operation is listed
+    if (!h_all_bytes) return SRPC_E_INVALID;
+    uint64_t total = 0;
+    int want = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (h_all_bytes[r] > ~0ull - total) return SRPC_E_INVALID;
+        total += h_all_bytes[r];
+        want += h_all_bytes[r] != 0;
+    }
+    if (h_all_bytes[root] != shard_bytes) return SRPC_E_INVALID;
+    if (total > root_cap) return SRPC_E_CAPACITY;
+    if (want > cap_ops) return SRPC_E_CAPACITY;
+    uint64_t off = 0;
+    int k = 0;
+    for (int r = 0; r < nranks; ++r) {
+        const uint64_t b = h_all_bytes[r];
+        if (b) ops[k++] = srpc_gather_op{r == root ? SRPC_GATHER_COPY : SRPC_GATHER_RECV, r, off, b};
+        off += b;
+    }
+    *nops = k;
+    return SRPC_OK;
+}
+
 int srpc_gather_wire(srpc_comm* c, const uint8_t* d_shard, uint64_t shard_bytes, uint8_t* d_root_wire,
                      uint64_t root_cap, const uint64_t* h_all_bytes, int root, void* stream) {
     if (!c || !c->comm || root < 0 || root >= c->nranks) return SRPC_E_INVALID;
     if (shard_bytes && !d_shard) return SRPC_E_INVALID;
+    // every argument checked (srpc_gather_plan) before the group is opened
+    std::vector<srpc_gather_op> ops(static_cast<size_t>(c->nranks));
+    int nops = 0;
+    if (int rc = srpc_gather_plan(c->rank, c->nranks, root, shard_bytes, h_all_bytes, root_cap, ops.data(),
+                                  c->nranks, &nops))
+        return rc;
+    if (nops == 0) return SRPC_OK;
+    if (c->rank == root && !d_root_wire) return SRPC_E_INVALID;
     auto s = static_cast<hipStream_t>(stream);
     DeviceGuard g(c->device);
-    if (c->rank != root) {
-        if (!shard_bytes) return SRPC_OK;
-        return nccl_rc(ncclSend(d_shard, shard_bytes, ncclUint8, root, c->comm, s));
-    }
-    // the root: every argument checked before the group is opened
-    if (!h_all_bytes) return SRPC_E_INVALID;
-    uint64_t total = 0;
-    for (int r = 0; r < c->nranks; ++r) {
-        if (h_all_bytes[r] > ~0ull - total) return SRPC_E_INVALID;
-        total += h_all_bytes[r];
-    }
-    if (h_all_bytes[root] != shard_bytes) return SRPC_E_INVALID;
-    if (total > root_cap) return SRPC_E_CAPACITY;
-    if (total && !d_root_wire) return SRPC_E_INVALID;
+    if (c->rank != root)  // one send, no group needed
+        return nccl_rc(ncclSend(d_shard, ops[0].bytes, ncclUint8, root, c->comm, s));
     if (ncclGroupStart() != ncclSuccess) return SRPC_E_HIP;
-    uint64_t off = 0;
     int rc = SRPC_OK;
-    for (int r = 0; r < c->nranks && rc == SRPC_OK; ++r) {
-        const uint64_t b = h_all_bytes[r];
-        if (b) {
-            if (r == root) {
-                if (hipMemcpyAsync(d_root_wire + off, d_shard, b, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                    rc = SRPC_E_HIP;
-            } else {
-                rc = nccl_rc(ncclRecv(d_root_wire + off, b, ncclUint8, r, c->comm, s));
-            }
+    for (int k = 0; k < nops && rc == SRPC_OK; ++k) {
+        const srpc_gather_op& op = ops[static_cast<size_t>(k)];
+        if (op.kind == SRPC_GATHER_COPY) {
+            if (hipMemcpyAsync(d_root_wire + op.offset, d_shard, op.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                rc = SRPC_E_HIP;
+        } else {
+            rc = nccl_rc(ncclRecv(d_root_wire + op.offset, op.bytes, ncclUint8, op.peer, c->comm, s));
         }
-        off += b;
     }
     return close_group(rc, &c, 1);
 }

@@ -53,27 +53,61 @@ def gather_packed(local, record_bytes: int, n: int, root: int = 0, group=None, c
         return local
     if comm is not None:  # the library's RCCL gather (production path)
         return comm.gather_wire(local, sizes, root)
+    # torch.distributed: the library's own plan (srpc_gather_plan, the list
+    # srpc_gather_wire enqueues) replayed as point-to-point operations
     out = None
     if rank == root:
         out = torch.empty(n * record_bytes, dtype=torch.uint8, device=local.device)
-    if all(s == sizes[0] for s in sizes):
-        parts = list(out.view(world, sizes[0]).unbind(0)) if rank == root else None
-        dist.gather(local, gather_list=parts, dst=root, group=group)
-        return out
-    ops = []
-    if rank == root:
-        for r, (lo, hi) in enumerate(ranges):
-            view = out[lo * record_bytes: hi * record_bytes]
-            if r == root:
-                view.copy_(local)
-            elif view.numel():
-                ops.append(dist.P2POp(dist.irecv, view, r, group))
-    elif local.numel():
-        ops.append(dist.P2POp(dist.isend, local, root, group))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+    run_gather_plan(gather_plan(rank, world, root, sizes[rank], sizes, n * record_bytes), local, out, group)
     return out
+
+
+def gather_plan(rank: int, nranks: int, root: int, shard_bytes: int, all_bytes, root_cap: int) -> list:
+    """srpc_gather_plan of the C ABI: the (kind, peer, offset, bytes) operations
+    rank ``rank`` of srpc_gather_wire enqueues, after the same argument checks
+    (raises SrpcError with SRPC_E_INVALID / SRPC_E_CAPACITY as it would)."""
+    import ctypes as C
+
+    from . import _lib
+    sizes = (C.c_uint64 * nranks)(*[int(b) for b in all_bytes]) if all_bytes is not None else None
+    ops = (_lib.GatherOp * nranks)()
+    k = C.c_int()
+    _lib.check(_lib.lib().srpc_gather_plan(rank, nranks, root, shard_bytes, sizes, root_cap, ops, nranks,
+                                           C.byref(k)), "srpc_gather_plan")
+    return [(ops[i].kind, ops[i].peer, ops[i].offset, ops[i].bytes) for i in range(k.value)]
+
+
+def run_gather_plan(ops, local, out, group=None, p2p: bool = True) -> None:
+    """Replays srpc_gather_plan's list over torch.distributed: SEND -> isend of
+    the shard, RECV -> irecv into out[offset:offset+bytes], COPY -> the root's
+    own shard.  ``p2p=False`` uses blocking send/recv in list order (gloo)."""
+    import torch.distributed as dist
+
+    from . import _lib
+    pending = []
+    for kind, peer, off, b in ops:
+        if kind == _lib.SRPC_GATHER_COPY:
+            out[off:off + b].copy_(local[:b])
+        elif kind == _lib.SRPC_GATHER_SEND:
+            pending.append(dist.P2POp(dist.isend, local[:b].contiguous(), peer, group) if p2p else
+                           ("send", local[:b].contiguous(), peer))
+        elif kind == _lib.SRPC_GATHER_RECV:
+            pending.append(dist.P2POp(dist.irecv, out[off:off + b], peer, group) if p2p else
+                           ("recv", out[off:off + b], peer))
+        else:
+            raise ValueError(f"unknown gather op kind {kind}")
+    if p2p:
+        if pending:
+            for w in dist.batch_isend_irecv(pending):
+                w.wait()
+        return
+    for what, t, peer in pending:
+        if what == "send":
+            dist.send(t, peer, group)
+        else:
+            buf = t.new_empty(t.shape)  # out[...] slices are views: receive, then place
+            dist.recv(buf, peer, group)
+            t.copy_(buf)
 
 
 class NativeComm:

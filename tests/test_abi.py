@@ -37,7 +37,7 @@ def test_library_exports_every_symbol():
 
 def test_library_loads_and_answers_host_calls():
     L = _lib.lib()
-    assert L.srpc_gpu_abi_version() == 7
+    assert L.srpc_gpu_abi_version() == 8
     assert L.srpc_status_string(-2) == b"device pointer misaligned"
     assert L.srpc_status_string(2).startswith(b"wire shorter")
     # argument validation needs no device

@@ -249,34 +249,126 @@ def test_host_pipe_pool_grows_with_concurrency_not_threads():
     assert not errs and hook(0) - base <= 4, (errs, hook(0) - base)
 
 
+def _hook(name, res, args):
+    import ctypes
+    fn = getattr(srpc_amd._lib.lib(), name)
+    fn.restype, fn.argtypes = res, args
+    return fn
+
+
+def test_host_pipes_not_shared_across_streams_while_busy():
+    """a pipe goes back to the pool when its call has been
+    enqueued, long before its copies finish.  A call on ANOTHER caller stream
+    must not take that busy pipe (its copies would queue behind the first
+    call's on the same internal streams); a call on the SAME stream may (its
+    work is ordered behind the first call's anyway); once the first call has
+    drained, any stream may reuse it."""
+    import ctypes
+    last = _hook("srpc_debug_host_last_pipe", ctypes.c_uint64, [])
+    kinds, p = plan("quad")
+    n, chunk = 1 << 22, 1 << 18            # 64 MiB each way: milliseconds of PCIe, microseconds to enqueue
+    cols = host_cols(kinds, n, np.random.default_rng(4))
+    want = bytes(oracle.pack(kinds, cols, n))
+    h_cols = [pinned(c) for c in cols]
+    wires = [pinned(np.zeros(len(want), np.uint8)) for _ in range(3)]
+    keep = [scratch_for(p, chunk, 3) for _ in range(3)]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    p.pack_host(h_cols, n, wires[0], chunk, keep[0][1], keep[0][2], depth=3, stream=s1)
+    a = last()
+    p.pack_host(h_cols, n, wires[1], chunk, keep[1][1], keep[1][2], depth=3, stream=s2)
+    b = last()
+    busy = not (s1.query())  # the first call was still moving bytes when the second borrowed
+    p.pack_host(h_cols, n, wires[2], chunk, keep[2][1], keep[2][2], depth=3, stream=s1)
+    c = last()
+    torch.cuda.synchronize()
+    for w in wires:
+        assert w.numpy().tobytes() == want
+    if busy:
+        assert a != b, "a busy pipe was lent to a call on another stream"
+    assert c == a, "a call on the same stream should reuse that stream's pipe"
+    p.pack_host(h_cols, n, wires[1], chunk, keep[1][1], keep[1][2], depth=3, stream=torch.cuda.Stream())
+    assert last() in (a, b), "an idle pipe should be reused, not a new one made"
+    torch.cuda.synchronize()
+
+
+def test_host_direct_accepts_host_registered_memory():
+    """direct mode on buffers pinned by hipHostRegister (mapped)
+    -- numpy memory the runtime did not allocate: the batch that fits is
+    accepted and exact, a batch longer than the registered range is refused."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    kinds, p = plan("quad")
+    n = 65_536
+    cols = host_cols(kinds, n, np.random.default_rng(6))
+    want = bytes(oracle.pack(kinds, cols, n))
+    page = 4096
+    raw = np.zeros(len(want) + 2 * page, np.uint8)
+    off = (-raw.ctypes.data) % page
+    wire = raw[off:off + len(want)]                       # page-aligned, exactly the batch
+    raw_cols = [np.zeros(c.nbytes + 2 * page, np.uint8) for c in cols]
+    reg_cols = []
+    for r, c in zip(raw_cols, cols):
+        o = (-r.ctypes.data) % page
+        v = r[o:o + c.nbytes]
+        v[:] = c.view(np.uint8)
+        reg_cols.append(v)
+    regs = [wire] + reg_cols
+    for a in regs:
+        assert hip.hipHostRegister(a.ctypes.data, a.nbytes, 2) == 0  # hipHostRegisterMapped
+    try:
+        p.pack_host([c.ctypes.data for c in reg_cols], n, wire.ctypes.data, 0, 0, 0, depth=1,
+                    wire_cap=len(want))
+        torch.cuda.synchronize()
+        assert wire.tobytes() == want
+        with pytest.raises(srpc_amd.SrpcError):   # one record more than the registered wire holds
+            p.pack_host([c.ctypes.data for c in reg_cols], n + 1, wire.ctypes.data, 0, 0, 0, depth=1,
+                        wire_cap=len(want) + 16)
+    finally:
+        torch.cuda.synchronize()
+        for a in regs:
+            hip.hipHostUnregister(a.ctypes.data)
+
+
 @pytest.mark.parametrize("direction", ["pack", "unpack"])
-def test_host_ring_error_drains_into_callers_stream(monkeypatch, direction):
-    """An error part way through the chunked ring (injected at chunk 14 of 16,
-    SRPC_HOST_FAIL_AT) returns it, and the caller's stream is ordered after
-    every copy the call already enqueued: once that stream is synchronized,
-    chunks 0..13 are complete in the host buffers."""
+def test_host_ring_error_drains_into_callers_stream(direction):
+    """An error part way through the chunked ring (injected at chunk 14 of 16
+    through the test hook srpc_debug_host_fail_at) returns it, and the caller's
+    stream is ordered after every copy the call already enqueued: once that
+    stream is synchronized, chunks 0..13 are complete in the host buffers."""
+    import ctypes
+    fail_at = _hook("srpc_debug_host_fail_at", None, [ctypes.c_uint64])
     kinds, p = plan("quad")
     n, chunk = 16 * 65_536, 65_536
     cols = host_cols(kinds, n, np.random.default_rng(3))
     want = bytes(oracle.pack(kinds, cols, n))
     keep, sp, sb = scratch_for(p, chunk, 3)
     s = torch.cuda.Stream()
-    monkeypatch.setenv("SRPC_HOST_FAIL_AT", "14")
+    fail_at(14)
     done = 14 * chunk
+    try:
+        if direction == "pack":
+            h_cols = [pinned(c) for c in cols]
+            h_wire = pinned(np.zeros(len(want), np.uint8))
+            with pytest.raises(srpc_amd.SrpcError):
+                p.pack_host(h_cols, n, h_wire, chunk, sp, sb, depth=3, stream=s)
+            s.synchronize()
+            assert h_wire[:done * 16].numpy().tobytes() == want[:done * 16]
+        else:
+            h_wire = pinned(np.frombuffer(want, np.uint8))
+            back = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
+            with pytest.raises(srpc_amd.SrpcError):
+                p.unpack_host(h_wire, len(want), n, back, chunk, sp, sb, depth=3, stream=s)
+            s.synchronize()
+            for b, c in zip(back, cols):
+                assert b[:done * c.itemsize].numpy().tobytes() == c.tobytes()[:done * c.itemsize]
+    finally:
+        fail_at(2**64 - 1)
+        torch.cuda.synchronize()
+    # disarmed: the same call succeeds
     if direction == "pack":
-        h_cols = [pinned(c) for c in cols]
-        h_wire = pinned(np.zeros(len(want), np.uint8))
-        with pytest.raises(srpc_amd.SrpcError):
-            p.pack_host(h_cols, n, h_wire, chunk, sp, sb, depth=3, stream=s)
+        p.pack_host(h_cols, n, h_wire, chunk, sp, sb, depth=3, stream=s)
         s.synchronize()
-        assert h_wire[:done * 16].numpy().tobytes() == want[:done * 16]
-    else:
-        h_wire = pinned(np.frombuffer(want, np.uint8))
-        back = [pinned(np.zeros(c.nbytes, np.uint8)) for c in cols]
-        with pytest.raises(srpc_amd.SrpcError):
-            p.unpack_host(h_wire, len(want), n, back, chunk, sp, sb, depth=3, stream=s)
-        s.synchronize()
-        for b, c in zip(back, cols):
-            assert b[:done * c.itemsize].numpy().tobytes() == c.tobytes()[:done * c.itemsize]
-    monkeypatch.delenv("SRPC_HOST_FAIL_AT")
-    torch.cuda.synchronize()
+        assert h_wire.numpy().tobytes() == want
