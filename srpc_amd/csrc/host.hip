@@ -258,19 +258,30 @@ bool mapped(const void* h, uint64_t bytes, void** d) {
         (void)hipGetLastError();
         return false;
     }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    uintptr_t lo = reinterpret_cast<uintptr_t>(*d);  // the range in the address space it was found in
-    if (hipMemGetAddressRange(&base, &size, *d) != hipSuccess || !base) {
-        (void)hipGetLastError();
-        if (hipMemGetAddressRange(&base, &size, const_cast<void*>(h)) != hipSuccess || !base) {
-            (void)hipGetLastError();
-            return false;
+    // the allocation's range, asked of the runtime four ways (hipHostMalloc
+    // blocks answer the first; hipHostRegister'ed ranges may answer only the
+    // pointer attributes), each in the address space it was asked in
+    const void* at_ptr[2] = {*d, h};
+    for (int i = 0; i < 4; ++i) {
+        const void* q = at_ptr[i & 1];
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        bool ok;
+        if (i < 2) {
+            ok = hipMemGetAddressRange(&base, &size, const_cast<void*>(q)) == hipSuccess;
+        } else {
+            ok = hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                                        reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(q))) == hipSuccess &&
+                 hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                                        reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(q))) == hipSuccess;
         }
-        lo = reinterpret_cast<uintptr_t>(h);
+        if (!ok) (void)hipGetLastError();
+        if (!ok || !base || !size) continue;
+        const uintptr_t b = reinterpret_cast<uintptr_t>(base), lo = reinterpret_cast<uintptr_t>(q);
+        if (lo < b || lo - b > size) continue;  // an answer about another range
+        return bytes <= size - (lo - b);
     }
-    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-    return lo >= b && lo - b <= size && bytes <= size - (lo - b);
+    return false;
 }
 
 __global__ void k_or_bounds(srpc_unpack_status* st, uint64_t at) {
