@@ -94,6 +94,8 @@ typedef struct srpc_unpack_status {
                                    other than the block's speculated start, bit 1 =
                                    it entered some block where no table slot was
                                    (that block was walked record by record),
+                                   bit 2 = the first scan met such a position and
+                                   the repair pass gave every block exit slots,
                                    bits 8-31 = scan waves that walked (saturating);
                                    0 from every other call                     */
     uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */

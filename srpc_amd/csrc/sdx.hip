@@ -85,8 +85,17 @@ constexpr uint32_t kX = 128;                     // landing slots per block
 constexpr uint32_t kX = 0;
 #endif
 constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
-constexpr uint32_t kEnt = kWin + 1 + kX;         // table entries per block: the window's, the extra slot,
-                                                 // then the landing slots
+// Exit slots (round 6, the repair pass): the live exits of every chain from
+// every position of the block before (and from longer records of blocks
+// further back), so the cursor's entry into a block is always a slot -- see
+// k_sx_fan / k_sx_exits.
+constexpr uint32_t kE = 64;                      // exit slots per block
+constexpr uint32_t kNear = 128;                  // a block's live exits into the next block, at most
+constexpr uint32_t kFarIn = 64;                  // exits of longer records a block receives, at most
+constexpr uint32_t kFarSet = 256;                // k_sx_fan's set of a block's far exits (LDS hash)
+constexpr uint32_t kXS = kX + kE;                // a wave's LDS copy of a block's landing + exit slots
+constexpr uint32_t kEnt = kWin + 1 + kX + kE;    // table entries per block: the window's, the extra slot,
+                                                 // the landing slots, then the exit slots
 constexpr uint32_t kHdr = 8;                     // header words per block
 constexpr uint32_t kRepairMin = 16;              // segments past which k_sx_spec repairs its chunks
 constexpr uint32_t kRepairMax = 16;              // repair passes at most
@@ -112,6 +121,8 @@ constexpr uint32_t kCtlOff = 1;      // entries that were not a block's primary 
 constexpr uint32_t kCtlTailOn = 2;   // the stream stopped before record n: the tail fill runs
 constexpr uint32_t kCtlT = 3;        // ... from record T
 constexpr uint32_t kCtlTot = 4;      // ... str_offs value per string ordinal (kMaxNC + 1 words)
+constexpr uint32_t kCtlRepair = 8;   // the first scan met a position no table holds: repair, scan again
+constexpr uint32_t kCtlOver = 9;     // blocks whose exit slots overflowed (diagnostics)
 constexpr uint32_t kCtlWords = 16;
 
 // stop bits: bit 0 = the chain stopped, bits 1-2 = why (SRPC_STATUS_PREFIX / _BOUNDS)
@@ -176,7 +187,8 @@ struct SxArgs {
     uint32_t gap[kMaxFields + 1];  // fixed bytes before string ordinal 0 (prefix included), between
                                    // strings k - 1 and k, after the last string (the parse's program)
     uint32_t mode;               // test hooks: 1 = tables hold only the first speculated start, 2 = empty
-                                 // tables, 4 = the exact filter at every position (A/B)
+                                 // tables, 4 = the exact filter at every position (A/B), 8 = no repair
+                                 // pass (a position no table holds is walked, as before round 6)
 };
 
 struct SxScratch {
@@ -190,6 +202,11 @@ struct SxScratch {
     uint64_t* ctl;   // kCtlWords
     uint16_t* rl;    // per block, kMaxRec slots: its chunks' record starts in order (offsets from the block)
     uint16_t* xp;    // per block, kX slots: its landing slots' positions (offsets from the block, ascending)
+    uint16_t* ep;    // per block, kE slots: its exit slots' positions (offsets from the block, ascending)
+    uint16_t* xnear; // per block, kNear: live exits of its chains into the next block (offsets there)
+    uint32_t* xnearc;  // per block: their count | overflow << 16
+    uint16_t* xin;   // per block, kFarIn: live exits into it of records from two or more blocks back
+    uint32_t* xinc;  // per block: their count (atomic; past kFarIn: overflow)
 };
 
 // A chain's result / the cursor's state: position (exit, or the next record
@@ -743,12 +760,27 @@ __device__ __forceinline__ int slot_of(uint64_t h0, uint64_t h1, uint64_t h3, ui
 __device__ __forceinline__ uint32_t h4_nx(uint64_t h4) { return static_cast<uint32_t>(h4 & 0xff); }
 __device__ __forceinline__ uint32_t h4_zr(uint64_t h4) { return static_cast<uint32_t>((h4 >> 16) & 0xffff); }
 __device__ __forceinline__ uint32_t h4_za(uint64_t h4) { return static_cast<uint32_t>((h4 >> 32) & 0xff); }
+// Header word 5: exit slots (0 until a repair pass gives the block some).
+__device__ __forceinline__ uint32_t h5_ne(uint64_t h5) { return static_cast<uint32_t>(h5 & 0xff); }
+// The landing slots a lookup uses (none in the test-hook table modes).
+__device__ __forceinline__ uint32_t nx_used(const SxArgs& a, uint64_t h4) { return (a.mode & 3) ? 0 : h4_nx(h4); }
+
+// First index in xs[0, n) whose value is >= v (xs ascending).
+__device__ __forceinline__ uint32_t lower16(const uint16_t* xs, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (xs[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
 
 // Where the cursor at x goes through block blk: the table entry `idx` (its
 // chain to the block's end), minus `sub` zero records (below), or idx < 0 (a
 // miss).  Beyond slot_of:
-// - the landing slots (xs: the block's ascending offsets, staged in LDS by
-//   the caller; a binary search per lane);
+// - the landing slots (xs[0, nx): the block's ascending offsets, staged in
+//   LDS by the caller; a binary search per lane);
 // - a run of zero bytes: when the block's bytes [za, x) are all zero (za:
 //   just past the window's last nonzero byte, header word 4), the schema has
 //   no prefix and its all-zero record (fixed_bytes = Z long, every string
@@ -756,46 +788,52 @@ __device__ __forceinline__ uint32_t h4_za(uint64_t h4) { return static_cast<uint
 //   parses as zero records up to x -- so w's chain passes through x and the
 //   chain from x is w's without its first (x - w) / Z records (no chars).  A
 //   record whose chars are zeros and that straddles the block's start ends
-//   there, whatever its length (its length field may lie in the window).
+//   there, whatever its length (its length field may lie in the window);
+// - the exit slots (xs[kX, kX + ne), after a repair pass; in every mode).
 struct Slot {
     int idx;
     uint32_t sub;
 };
 __device__ __forceinline__ Slot find_slot(const SxArgs& a, uint64_t h0, uint64_t h1, uint64_t h3, uint32_t meta,
-                                          uint64_t h4, const uint16_t* xs, uint64_t b0, uint64_t x) {
+                                          uint64_t h4, uint64_t h5, const uint16_t* xs, uint64_t b0, uint64_t x) {
     Slot r{slot_of(h0, h1, h3, meta & 0xff, b0, x), 0};
-    if (r.idx >= 0 || (a.mode & 3)) return r;
+    if (r.idx >= 0) return r;
     const uint64_t off = x - b0;
-    const uint32_t nx = kX ? h4_nx(h4) : 0;
-    if (kX && nx && off < kSB) {
-        uint32_t lo = 0, hi = nx;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (xs[m] < off) lo = m + 1;
-            else hi = m;
+    if (!(a.mode & 3)) {
+        const uint32_t nx = kX ? h4_nx(h4) : 0;
+        if (kX && nx && off < kSB) {
+            const uint32_t lo = lower16(xs, nx, static_cast<uint32_t>(off));
+            if (lo < nx && xs[lo] == off) {
+                r.idx = static_cast<int>(kWin + 1 + lo);
+                return r;
+            }
         }
-        if (lo < nx && xs[lo] == off) {
-            r.idx = static_cast<int>(kWin + 1 + lo);
-            return r;
+        const uint32_t Z = a.fixed_bytes, za = h4_za(h4);
+        if (!a.prefix_len && Z <= kWin && off >= za && off <= h4_zr(h4)) {
+            const uint32_t wo = za + static_cast<uint32_t>((off - za) % Z);
+            if (wo < kWin && ((h0 >> wo) & 1)) {
+                r.idx = __builtin_popcountll(h0 & ((1ull << wo) - 1));
+                r.sub = static_cast<uint32_t>((off - wo) / Z);
+                return r;
+            }
         }
     }
-    const uint32_t Z = a.fixed_bytes, za = h4_za(h4);
-    if (!a.prefix_len && Z <= kWin && off >= za && off <= h4_zr(h4)) {
-        const uint32_t wo = za + static_cast<uint32_t>((off - za) % Z);
-        if (wo < kWin && ((h0 >> wo) & 1)) {
-            r.idx = __builtin_popcountll(h0 & ((1ull << wo) - 1));
-            r.sub = static_cast<uint32_t>((off - wo) / Z);
-        }
+    const uint32_t ne = h5_ne(h5);
+    if (ne && off < kSB) {
+        const uint32_t lo = lower16(xs + kX, ne, static_cast<uint32_t>(off));
+        if (lo < ne && xs[kX + lo] == off) r.idx = static_cast<int>(kWin + 1 + kX + lo);
     }
     return r;
 }
 
-// The wave's LDS copy of block blk's landing slots (wave-uniform blk; every
-// lane takes part).
-__device__ __forceinline__ void stage_xs(const SxScratch& S, uint64_t blk, uint32_t nx, uint16_t* xs) {
-    if constexpr (kX == 0) return;
+// The wave's LDS copy of block blk's landing slots (xs[0, nx)) and exit slots
+// (xs[kX, kX + ne)); wave-uniform blk; every lane takes part.
+__device__ __forceinline__ void stage_xs(const SxScratch& S, uint64_t blk, uint32_t nx, uint32_t ne, uint16_t* xs) {
+    if (!nx && !ne) return;
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t i = lane; i < nx; i += 64) xs[i] = S.xp[blk * kX + i];
+    if constexpr (kX > 0)
+        for (uint32_t i = lane; i < nx; i += 64) xs[i] = S.xp[blk * kX + i];
+    for (uint32_t i = lane; i < ne; i += 64) xs[kX + i] = S.ep[blk * kE + i];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
@@ -1182,7 +1220,10 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
     const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
     SXP_BEGIN
     if (b == 0 && tid < kCtlWords) S.ctl[tid] = 0;  // this call's counters (read by the later launches)
-    if (tid == 0) L.s_nx = 0;
+    if (tid == 0) {
+        L.s_nx = 0;
+        S.xinc[b] = 0;  // (the repair pass's inbox of this block, if it runs)
+    }
     const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1, kPre);
     const StageOnlyRd so{rd};
     SXP(0);
@@ -1477,8 +1518,240 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
         h[1] = sF;
         h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull) |
                (static_cast<uint64_t>(min<uint32_t>(C.pcnt[kBlock], kMaxRec)) << 32);
+        h[5] = 0;  // no exit slots (until a repair pass)
     }
     SXP(3);
+}
+
+// ---- the repair pass (round 6): exit slots -----------------------------------------
+// Run only after the first scan met a position no table holds (ctl
+// kCtlRepair; otherwise every workgroup reads one word and ends).  The
+// reference's cursor enters block c at the end of the record that straddles
+// c's start: a record that starts at a position of block c - 1 (or further
+// back) the cursor reaches.  k_sx_fan takes EVERY position p of a block b:
+// the record at p, parsed in full (where one parses), links p to the next
+// record start; pointer jumping over those links in LDS (in place, at most
+// log2 of the records a block holds + 1 rounds) gives every p its exit from
+// the block -- the first record start past the block's end -- or a stop.  The
+// distinct exits at which a record parses ("live": a cursor entering anywhere
+// else stops right there, one parse) are then EVERY position the cursor can
+// enter block b + 1 at (or a later block, for a record longer than a block),
+// whatever the speculation made of block b's bytes.  k_sx_exits makes them
+// the target block's exit slots: each one's chain through the block, like the
+// table's other slots.  The second scan then meets a position no table holds
+// only where a block's exits overflowed (kNear, kFarIn, kE) or the wire is 4
+// GiB or longer: it walks those, as every miss was walked before round 6.
+// Cost: one parse per position (most stop at the first length) and the
+// jumping, for every block, in parallel -- O(bytes), no serial chain of
+// blocks.  Both kernels take blocks grid-stride from a bounded grid, so on
+// the (usual) calls that need no repair they cost two short launches.
+constexpr uint32_t kJStop = 0xFFFFFFFFu;
+static_assert(kFarSet == 256 && kSB / 32 == kBlock, "one bitmap word / one hash slot per thread");
+
+struct FanLds {
+    alignas(16) uint8_t st[kStage + 16];
+    alignas(16) uint8_t pre[kMaxPrefix + 16];
+    uint32_t J[kSB];           // per position: the next record start (< kSB: in the block), its exit, or kJStop
+    uint32_t nearm[kSB / 32];  // exits into the next block (a bit per position)
+    uint32_t far[kFarSet];     // exits past the next block, offsets from this block (0 = empty slot)
+    uint64_t ws[kBlock / 64];
+    uint32_t far_over;
+};
+
+// A record parses at x (read through the stage where it holds x).
+template <class Rd>
+__device__ __forceinline__ bool live_at(const SxArgs& a, const Rd& rd, uint64_t x) {
+    if (!filter(a, rd, x)) return false;
+    uint32_t err;
+    uint64_t t[kMaxNC + 1];
+    (void)parse_rd<0>(a, rd, x, &err, t);
+    return !err;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_fan(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+    if (!S.ctl[kCtlRepair]) return;
+    __shared__ FanLds L;
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t b = blockIdx.x; b + 1 < a.nb; b += gridDim.x) {
+        const uint64_t b0 = b * kSB, b1 = b0 + kSB;  // (never the last block: a whole one)
+        if (a.W >= kJStop) {  // offsets in 32 bits: beyond, the second scan walks
+            if (tid == 0) S.xnearc[b] = 0;
+            continue;
+        }
+        L.nearm[tid] = 0;
+        L.far[tid] = 0;
+        if (tid == 0) L.far_over = 0;
+        const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);  // (ends in a barrier)
+        // the record at every position: its end, relative to b0
+        for (uint32_t i = tid; i < kSB; i += kBlock) {
+            const uint64_t p = b0 + i;
+            uint32_t v = kJStop;
+            if (filter(a, rd, p)) {
+                uint32_t err;
+                uint64_t t[kMaxNC + 1];
+                const uint64_t q = parse_rd<0>(a, rd, p, &err, t);
+                if (!err) v = static_cast<uint32_t>(q - b0);
+            }
+            L.J[i] = v;
+        }
+        __syncthreads();
+        // pointer jumping: a link inside the block is replaced by its target's
+        // (a concurrent reader sees either, both on the same chain)
+        for (uint32_t r = 0; r < 32; ++r) {
+            bool more = false;
+            for (uint32_t i = tid; i < kSB; i += kBlock) {
+                uint32_t v = L.J[i];
+                if (v < kSB) {
+                    v = L.J[v];
+                    L.J[i] = v;
+                    more |= v < kSB;
+                }
+            }
+            if (!__syncthreads_or(more)) break;
+        }
+        // the distinct exits: the next block's in a bitmap, later ones in a set
+        for (uint32_t i = tid; i < kSB; i += kBlock) {
+            const uint32_t v = L.J[i];
+            if (v == kJStop || v < kSB) continue;
+            const uint64_t x = b0 + v;
+            if (x >= a.W) continue;  // the wire's end: no block to enter
+            if (x < b1 + kSB) {
+                atomicOr(&L.nearm[(x - b1) >> 5], 1u << ((x - b1) & 31));
+            } else {
+                uint32_t h = (v * 2654435761u) >> 24, k = 0;
+                for (; k < kFarSet; ++k) {
+                    const uint32_t old = atomicCAS(&L.far[h], 0u, v);
+                    if (old == 0u || old == v) break;
+                    h = (h + 1) & (kFarSet - 1);
+                }
+                if (k == kFarSet) L.far_over = 1;
+            }
+        }
+        __syncthreads();
+        // the next block's live exits, in order (a bitmap word per thread)
+        uint32_t m = L.nearm[tid], live = 0;
+        while (m) {
+            const uint32_t bit = __builtin_ctz(m);
+            m &= m - 1;
+            if (live_at(a, rd, b1 + 32 * tid + bit)) live |= 1u << bit;
+        }
+        uint64_t tot;
+        uint64_t k = block_xscan(__builtin_popcount(live), &tot, L.ws);
+        while (live) {
+            const uint32_t bit = __builtin_ctz(live);
+            live &= live - 1;
+            if (k < kNear) S.xnear[b * kNear + k] = static_cast<uint16_t>(32 * tid + bit);
+            ++k;
+        }
+        // the later blocks' live exits, into their inboxes (a set slot per thread)
+        const uint32_t v = L.far[tid];
+        if (v) {
+            const uint64_t x = b0 + v;
+            if (live_at(a, rd, x)) {
+                const uint64_t t = x / kSB;
+                const uint32_t j = atomicAdd(&S.xinc[t], 1u);
+                if (j < kFarIn) S.xin[t * kFarIn + j] = static_cast<uint16_t>(x - t * kSB);
+            }
+        }
+        if (tid == 0) {
+            S.xnearc[b] = static_cast<uint32_t>(min<uint64_t>(tot, kNear)) | (tot > kNear ? 1u << 16 : 0u);
+            if (L.far_over) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOver]), 1ull);
+        }
+        __syncthreads();  // (the next block's stage overwrites this one's LDS)
+    }
+}
+
+template <int NC>
+struct ExitLds {
+    alignas(16) uint8_t st[kStage + 16];
+    alignas(16) uint8_t pre[kMaxPrefix + 16];
+    Chunks<NC> c;
+    uint16_t xs[kXS];                 // the block's landing slots, then (kX on) its exit slots
+    uint16_t cand[kNear + kFarIn];
+    uint16_t keep[kNear + kFarIn];
+    uint8_t first[kNear + kFarIn];
+    uint32_t nkeep;
+};
+static_assert(kNear + kFarIn <= kBlock, "a thread per candidate");
+
+// Block c's exit slots: the live exits of block c - 1's chains into it and of
+// longer records' into it (k_sx_fan), minus the positions its table already
+// holds, sorted, at most kE; each one's chain through the block, as the
+// table's other chains (the chunks walked again from phase 1's starts).
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+    if (!S.ctl[kCtlRepair]) return;
+    __shared__ ExitLds<NC> L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint64_t c = 1 + blockIdx.x; c < a.nb; c += gridDim.x) {
+        const uint32_t xn = S.xnearc[c - 1], fin = S.xinc[c];
+        const uint32_t nn = min<uint32_t>(xn & 0xffff, kNear), nf = min<uint32_t>(fin, kFarIn), nc = nn + nf;
+        if (nc == 0) continue;  // (uniform: every thread read the same words)
+        const uint64_t b0 = c * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
+        if (tid < nc) L.cand[tid] = tid < nn ? S.xnear[(c - 1) * kNear + tid] : S.xin[c * kFarIn + (tid - nn)];
+        if (tid == 0) L.nkeep = 0;
+        const uint64_t* h = S.hdr + kHdr * c;
+        const uint64_t h0 = h[0], h1 = h[1], h3 = h[3], h4 = h[4];
+        const uint32_t meta = static_cast<uint32_t>(h[2]), nx = nx_used(a, h4);
+        for (uint32_t i = tid; i < nx; i += kBlock) L.xs[i] = S.xp[c * kX + i];
+        const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);  // (ends in a barrier)
+        // the chunks from phase 1's (repaired) starts, linked into segments
+        const uint64_t clo = b0 + static_cast<uint64_t>(tid) * kSC, chi = min<uint64_t>(clo + kSC, b1);
+        const uint8_t sb = clo < b1 ? S.spec[c * kBlock + tid] : kNoSpec;
+        const uint64_t sp = sb == kNoSpec ? ~0ull : clo + sb;
+        uint64_t cch[kMaxNC + 1] = {};
+        uint32_t ccnt, cstop;
+        uint64_t cexit;
+        walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
+        Chunks<NC>& C = L.c;
+        C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
+        C.exit[tid] = cexit;
+        C.stop[tid] = static_cast<uint8_t>(cstop);
+        const uint64_t hm = __ballot(sp != ~0ull);
+        if (lane == 0) C.has[tid >> 6] = hm;
+        __syncthreads();
+        link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);  // (ends in a barrier)
+        // the candidates the table does not hold yet
+        if (tid < nc) {
+            const uint32_t o = L.cand[tid];
+            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0) {
+                const uint32_t k = atomicAdd(&L.nkeep, 1u);
+                L.keep[k] = static_cast<uint16_t>(o);
+            }
+        }
+        __syncthreads();
+        const uint32_t nk = L.nkeep;
+        // sorted, duplicates dropped (a near exit can also arrive as a far one)
+        uint32_t mine = 0;
+        if (tid < nk) {
+            mine = L.keep[tid];
+            bool first = true;
+            for (uint32_t k = 0; k < tid; ++k) first &= L.keep[k] != mine;
+            L.first[tid] = first ? 1 : 0;
+        }
+        __syncthreads();
+        uint32_t ne = 0;
+        if (tid < nk && L.first[tid]) {
+            uint32_t rank = 0;
+            for (uint32_t k = 0; k < nk; ++k) rank += L.first[k] && L.keep[k] < mine;
+            if (rank < kE) L.xs[kX + rank] = static_cast<uint16_t>(mine);
+        }
+        ne = static_cast<uint32_t>(__syncthreads_count(tid < nk && L.first[tid]));
+        const uint32_t nu = min(ne, kE);
+        for (uint32_t k = tid; k < nu; k += kBlock) {
+            const uint32_t o = L.xs[kX + k];
+            st_store<NC>(S.ent + (c * kEnt + kWin + 1 + kX + k) * ew<NC>(),
+                         walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
+            S.ep[c * kE + k] = static_cast<uint16_t>(o);
+        }
+        if (tid == 0) {
+            const bool over = ne > kE || (xn >> 16) || fin > kFarIn;
+            S.hdr[kHdr * c + 5] = nu | (over ? 1u << 8 : 0u);
+            if (over) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOver]), 1ull);
+        }
+        __syncthreads();  // (the next block's stage overwrites this one's LDS)
+    }
 }
 
 // ---- phase 2: the scan of the tables ----------------------------------------------
@@ -1489,7 +1762,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
 // the primary chains' records and chars (inclusive prefix sums over the lanes).
 template <int NC>
 struct Held {
-    uint64_t h0, h1, h3, h4;
+    uint64_t h0, h1, h3, h4, h5;
     uint32_t meta;  // slots | primary << 8
     uint64_t e[kKeep][ew<NC>()];
     bool has_prim;
@@ -1498,7 +1771,7 @@ struct Held {
     uint32_t run;                       // the last block of the run of primary links from this one
     __device__ __forceinline__ void load(const SxScratch& S, uint64_t blk, bool ok, uint32_t nbk) {
         const uint32_t lane = threadIdx.x & 63;
-        h0 = h4 = 0;
+        h0 = h4 = h5 = 0;
         h1 = h3 = ~0ull;
         meta = 0;
         has_prim = false;
@@ -1509,6 +1782,7 @@ struct Held {
             h1 = h[1];
             h3 = h[3];
             h4 = h[4];
+            h5 = h[5];
             meta = static_cast<uint32_t>(h[2]);
             const uint32_t ns = meta & 0xff, prim = (meta >> 8) & 0xff;
 #pragma unroll
@@ -1574,6 +1848,7 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
                                               bool may_walk = true) {
     // the held words of lane l (uniform reads, every lane takes part)
     const uint64_t h0 = rl64(hv.h0, l), h1 = rl64(hv.h1, l), h3 = rl64(hv.h3, l), h4 = rl64(hv.h4, l);
+    const uint64_t h5 = rl64(hv.h5, l);
     const uint32_t meta = __builtin_amdgcn_readlane(hv.meta, l);
     uint64_t e[kKeep][ew<NC>()];
 #pragma unroll
@@ -1583,9 +1858,8 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
     const uint64_t b0 = blk * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
     // a block no record starts in (the cursor is past its end) passes the state on
     const bool act = !st_done(s, a.W) && s.x < b1;
-    const uint32_t nx = h4_nx(h4);
-    if (nx && !(a.mode & 3) && __ballot(act)) stage_xs(S, blk, nx, xs);
-    const Slot sl = act ? find_slot(a, h0, h1, h3, meta, h4, xs, b0, s.x) : Slot{0, 0};
+    if (__ballot(act)) stage_xs(S, blk, nx_used(a, h4), h5_ne(h5), xs);
+    const Slot sl = act ? find_slot(a, h0, h1, h3, meta, h4, h5, xs, b0, s.x) : Slot{0, 0};
     const bool walk = act && sl.idx < 0 && may_walk;
     // every lane of the wave takes part in the staging of walk_miss
     St<NC> mw{};
@@ -1618,15 +1892,22 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
 }
 
 // A wave per group: for every slot of the group's first block -- window
-// slots, the extra slot, landing slots -- the chain through the group's blocks
-// (the group's table, indexed like the first block's).  Only the primary
-// slot's chain is walked where it meets no slot; any other chain that does is
-// given up (kDead): a start the block speculated wrongly that runs into
-// positions no table holds would otherwise cost a walk in every later block,
-// and the cursor enters a group there rarely (k_sx_top then takes that group
-// block by block).
+// slots, the extra slot, landing slots, exit slots -- the chain through the
+// group's blocks (the group's table, indexed like the first block's).  A
+// chain that meets a position no table holds is given up (kDead): in the
+// first scan (pass 0) every such chain -- the cursor that meets one sends the
+// call through the repair pass, which makes such positions slots -- and in
+// the second (pass 1, only after a repair) every chain but the primary
+// slot's, which is walked (a start the block speculated wrongly that runs
+// into positions no table holds would otherwise cost a walk in every later
+// block, and the cursor enters a group there rarely: k_sx_top then takes
+// that group block by block).  Test-hook mode 8 (no repair): pass 0 walks the
+// primary chains, as pass 1 does.
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+__global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                                      uint32_t pass) {
+    if (pass && !S.ctl[kCtlRepair]) return;  // (the second scan runs only after a repair)
+    const bool walk_prim = pass || (a.mode & 8);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
     if (g >= a.ng) return;
@@ -1637,21 +1918,24 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     const uint32_t meta0 = __builtin_amdgcn_readlane(hv.meta, 0);
     const uint32_t ns0 = meta0 & 0xff, prim0 = (meta0 >> 8) & 0xff;
     const bool has3 = rl64(hv.h3, 0) != ~0ull;
-    const uint32_t nx0 = (a.mode & 3) ? 0 : h4_nx(rl64(hv.h4, 0));
-    const uint32_t total = ns0 + (has3 ? 1 : 0) + nx0;
+    const uint32_t nx0 = nx_used(a, rl64(hv.h4, 0)), ne0 = h5_ne(rl64(hv.h5, 0));
+    const uint32_t total = ns0 + (has3 ? 1 : 0) + nx0 + ne0;
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
-    __shared__ uint16_t xss[kBlock / 64][kXA];
+    __shared__ uint16_t xss[kBlock / 64][kXS];
     uint8_t* stage = stages[threadIdx.x >> 6];
     __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
     uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     uint64_t* q = S.gp + g * (kHdr + ew<NC>());
     for (uint32_t k0 = 0; k0 < total; k0 += 64) {
-        // lane -> slot index: window slots, then the extra slot, then the landing slots
+        // lane -> slot index: window slots, the extra slot, the landing slots, the exit slots
         const uint32_t k = k0 + lane;
         const bool act = k < total;
         uint32_t idx = k;
-        if (k >= ns0) idx = has3 && k == ns0 ? kWin : kWin + 1 + (k - ns0 - (has3 ? 1 : 0));
+        if (k >= ns0) {
+            const uint32_t r = k - ns0 - (has3 ? 1 : 0);  // (for k past the extra slot)
+            idx = has3 && k == ns0 ? kWin : r < nx0 ? kWin + 1 + r : kWin + 1 + kX + (r - nx0);
+        }
         St<NC> s{};
         s.stop = 1;  // lanes past the slots stay put
         if (act) s = st_load<NC>(S.ent + (bf * kEnt + idx) * ew<NC>());
@@ -1663,18 +1947,19 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
             const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
             if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
             St<NC> t = s;
-            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs, primary);
+            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs,
+                              primary && walk_prim);
             if (act) s = t;
         }
         if (act) st_store<NC>(S.gent + (g * kEnt + idx) * ew<NC>(), s);
         if (primary) st_store<NC>(q + kHdr, s);  // what the in-order pass reads first
     }
     // the first block's header words, with the primary chain above: one record
-    if (lane < 5) {
-        const uint64_t hw[5] = {rl64(hv.h0, 0), rl64(hv.h1, 0), meta0, rl64(hv.h3, 0), rl64(hv.h4, 0)};
+    if (lane < 6) {
+        const uint64_t hw[6] = {rl64(hv.h0, 0), rl64(hv.h1, 0), meta0, rl64(hv.h3, 0), rl64(hv.h4, 0), rl64(hv.h5, 0)};
         uint64_t v = hw[0];
 #pragma unroll
-        for (uint32_t i = 1; i < 5; ++i) v = lane == i ? hw[i] : v;
+        for (uint32_t i = 1; i < 6; ++i) v = lane == i ? hw[i] : v;
         q[lane] = v;
     }
 }
@@ -1685,16 +1970,22 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
 // in no slot of the group's first block, or past that block, takes the group
 // block by block.  Then the stream's end: T, rec_offs[T], str_offs[.][T], the
 // status and the tail fill's parameters for k_sx_decode.
+// Pass 0 walks nothing: at the first position no table holds (or a group
+// chain given up there) it asks for the repair pass (ctl kCtlRepair) and
+// ends, writing nothing; pass 1 runs only after a repair and walks what is
+// still missing (a block whose exit slots overflowed).  Mode 8: pass 0 walks.
 template <int NC, bool kDecode>
 __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
-                                               srpc_unpack_status* st) {
+                                               srpc_unpack_status* st, uint32_t pass) {
+    if (pass && !S.ctl[kCtlRepair]) return;
+    const bool may_walk = pass || (a.mode & 8);
     constexpr uint32_t E = ew<NC>();
     constexpr uint32_t R = kHdr + E;  // words of a group's record in S.gp
     const uint32_t lane = threadIdx.x;
     const uint64_t W = a.W;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
     __shared__ Chunks<NC> mch;  // walk_miss's chunks
-    __shared__ uint16_t xs[kXA];
+    __shared__ uint16_t xs[kXS];
     St<NC> s{};
     bool miss = false, off = false;
     // lane l: group base + l -- its first block's header and the group's
@@ -1703,13 +1994,13 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
     auto fetch = [&](uint64_t base) {
         const uint64_t g = base + lane;
 #pragma unroll
-        for (uint32_t j = 0; j < R; ++j) nq[j] = g < a.ng && (j < 5 || j >= kHdr) ? S.gp[g * R + j] : 0;
+        for (uint32_t j = 0; j < R; ++j) nq[j] = g < a.ng && (j < 6 || j >= kHdr) ? S.gp[g * R + j] : 0;
     };
     fetch(0);
     for (uint64_t base = 0; base < a.ng; base += 64) {
         const uint32_t cnt = static_cast<uint32_t>(min<uint64_t>(64, a.ng - base));
         const uint64_t g = base + lane;
-        const uint64_t h0 = nq[0], h1 = nq[1], h3 = nq[3], h4 = nq[4];
+        const uint64_t h0 = nq[0], h1 = nq[1], h3 = nq[3], h4 = nq[4], h5 = nq[5];
         const uint32_t meta = static_cast<uint32_t>(nq[2]);
         St<NC> pe = st_load<NC>(nq + kHdr);  // the group's chain from its primary slot (its first block's sF = h1)
         fetch(base + 64);
@@ -1738,6 +2029,7 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
         while (l < cnt) {
             const uint64_t gl = base + l;
             const uint64_t lh0 = rl64(h0, l), lh1 = rl64(h1, l), lh3 = rl64(h3, l), lh4 = rl64(h4, l);
+            const uint64_t lh5 = rl64(h5, l);
             const uint32_t lmeta = __builtin_amdgcn_readlane(meta, l);
             const uint32_t lprim = (lmeta >> 8) & 0xff;
             if (!st_done(s, W) && lprim != kNoPrim && s.x == lh1) {
@@ -1768,6 +2060,10 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
                 t.stop = __builtin_amdgcn_readlane(pe.stop, m);
                 s = t;
                 l = m + 1;
+                if (!may_walk && s.stop == kDead) {  // a primary chain given up: repair first
+                    if (lane == 0) S.ctl[kCtlRepair] = 1;
+                    return;
+                }
                 continue;
             }
             {
@@ -1783,9 +2079,8 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
             if (s.x >= min<uint64_t>(bend * kSB, W)) continue;  // the whole group lies inside one record
             const uint64_t blk = s.x / kSB;
             if (blk == bf) {
-                const uint32_t nx = h4_nx(lh4);
-                if (nx && !(a.mode & 3)) stage_xs(S, bf, nx, xs);
-                const Slot sl = find_slot(a, lh0, lh1, lh3, lmeta, lh4, xs, bf * kSB, s.x);
+                stage_xs(S, bf, nx_used(a, lh4), h5_ne(lh5), xs);
+                const Slot sl = find_slot(a, lh0, lh1, lh3, lmeta, lh4, lh5, xs, bf * kSB, s.x);
                 if (sl.idx >= 0) {
                     St<NC> e = st_load<NC>(S.gent + (gl * kEnt + sl.idx) * E);
                     if (e.stop != kDead) {  // (the primary slot's is taken above)
@@ -1801,16 +2096,19 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
                 const uint64_t b0 = j * kSB, b1 = min<uint64_t>(b0 + kSB, W);
                 if (s.x >= b1) continue;
                 const uint64_t* h = S.hdr + kHdr * j;
-                const uint64_t m = h[2], hj4 = h[4];
-                const uint32_t nx = h4_nx(hj4);
-                if (nx && !(a.mode & 3)) stage_xs(S, j, nx, xs);
-                const Slot sl = find_slot(a, h[0], h[1], h[3], static_cast<uint32_t>(m), hj4, xs, b0, s.x);
+                const uint64_t m = h[2], hj4 = h[4], hj5 = h[5];
+                stage_xs(S, j, nx_used(a, hj4), h5_ne(hj5), xs);
+                const Slot sl = find_slot(a, h[0], h[1], h[3], static_cast<uint32_t>(m), hj4, hj5, xs, b0, s.x);
                 if (sl.idx != static_cast<int>((m >> 8) & 0xff) || sl.sub) off = true;
                 if (sl.idx >= 0) {
                     St<NC> t = st_load<NC>(S.ent + (j * kEnt + sl.idx) * E);
                     t.cnt -= sl.sub;
                     st_add<NC>(s, t);
                 } else {
+                    if (!may_walk) {  // a position no table holds: repair first
+                        if (lane == 0) S.ctl[kCtlRepair] = 1;
+                        return;
+                    }
                     st_add<NC>(s, walk_miss<NC>(a, w, S, j, stage, mch, b0, b1, s.x, true));
                     miss = true;
                 }
@@ -1875,7 +2173,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
     St<NC> s = st_load<NC>(S.gin + g * E);
     uint64_t out[E];
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
-    __shared__ uint16_t xss[kBlock / 64][kXA];
+    __shared__ uint16_t xss[kBlock / 64][kXS];
     uint8_t* stage = stages[threadIdx.x >> 6];
     __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
     uint16_t* xs = xss[threadIdx.x >> 6];
@@ -1960,8 +2258,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
         }
     }
     if (b == 0 && tid == 0 && st && kDecode) {  // diagnostics (srpc_unpack_status.reserved)
-        const uint64_t miss = S.ctl[kCtlMiss], off = S.ctl[kCtlOff];
-        st->reserved = (off ? 1u : 0u) | (miss ? 2u : 0u) | (static_cast<uint32_t>(min<uint64_t>(miss, 0xffffff)) << 8);
+        const uint64_t miss = S.ctl[kCtlMiss], off = S.ctl[kCtlOff], rep = S.ctl[kCtlRepair];
+        st->reserved = (off ? 1u : 0u) | (miss ? 2u : 0u) | (rep ? 4u : 0u) |
+                       (static_cast<uint32_t>(min<uint64_t>(miss, 0xffffff)) << 8);
     }
     if (b >= a.nb) return;
     const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
@@ -2271,7 +2570,7 @@ __global__ void k_zero_ctl(uint64_t* ctl) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct SxLayout {
-    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, xp, total;
+    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, xp, ep, xnear, xnearc, xin, xinc, total;
 };
 
 SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
@@ -2300,6 +2599,16 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     o += r256(2 * kMaxRec * L.nb);
     L.xp = o;
     o += r256(2 * kX * L.nb);
+    L.ep = o;
+    o += r256(2 * kE * L.nb);
+    L.xnear = o;
+    o += r256(2 * kNear * L.nb);
+    L.xnearc = o;
+    o += r256(4 * L.nb);
+    L.xin = o;
+    o += r256(2 * kFarIn * L.nb);
+    L.xinc = o;
+    o += r256(4 * L.nb);
     L.total = o;
     return L;
 }
@@ -2313,8 +2622,17 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
     if (a.nb) launch(k_sx_spec<NC>, dim3(a.nb), dim3(kBlock), 0, s, a, wire, S);
     else hipLaunchKernelGGL(k_zero_ctl, dim3(1), dim3(64), 0, s, S.ctl);
     const uint32_t gw = (a.ng + kBlock / 64 - 1) / (kBlock / 64);
-    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
-    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st);
+    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, 0u);
+    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
+    // the repair pass and the second scan: each workgroup reads one control
+    // word and ends unless the first scan asked for them (a bounded grid)
+    if (a.nb > 1) {
+        const uint32_t rg = static_cast<uint32_t>(std::min<uint64_t>(a.nb, 1024));
+        launch(k_sx_fan<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
+        launch(k_sx_exits<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
+    }
+    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, 1u);
+    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 1u);
     if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
     const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
     launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
@@ -2367,7 +2685,12 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
                 reinterpret_cast<uint64_t*>(base + SL.bst),
                 reinterpret_cast<uint64_t*>(base + SL.ctl),
                 reinterpret_cast<uint16_t*>(base + SL.rl),
-                reinterpret_cast<uint16_t*>(base + SL.xp)};
+                reinterpret_cast<uint16_t*>(base + SL.xp),
+                reinterpret_cast<uint16_t*>(base + SL.ep),
+                reinterpret_cast<uint16_t*>(base + SL.xnear),
+                reinterpret_cast<uint32_t*>(base + SL.xnearc),
+                reinterpret_cast<uint16_t*>(base + SL.xin),
+                reinterpret_cast<uint32_t*>(base + SL.xinc)};
     SxArgs a{};
     uint32_t si = 0;
     for (uint32_t f = 0; f < p->nfields; ++f) {
@@ -2419,10 +2742,11 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
 }  // extern "C"
 
 // Test hook (not part of the C ABI in include/), bits: 1 = block tables hold
-// only the first speculated start (every other entry is walked from global
-// memory), 2 = empty tables (every block entered is walked), 4 = the
-// speculation's exact filter at every position instead of zero-byte
-// candidates; 0 = normal.  Returns the previous setting.
+// only the first speculated start (every other entry needs the repair pass's
+// exit slots, or a walk), 2 = empty tables (every block entered needs them),
+// 4 = the speculation's exact filter at every position instead of zero-byte
+// candidates, 8 = no repair pass (a position no table holds is walked, the
+// round-5 path); 0 = normal.  Returns the previous setting.
 #ifdef SRPC_SX_PHASES
 extern "C" int srpc_debug_sx_phases(void* d_buf, uint64_t nblocks) {
     unsigned long long* p = static_cast<unsigned long long*>(d_buf);
@@ -2434,5 +2758,5 @@ extern "C" int srpc_debug_sx_phases(void* d_buf, uint64_t nblocks) {
 #endif
 
 extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_tables(int mode) {
-    return static_cast<int>(srpc_impl::g_sx_mode.exchange(static_cast<uint32_t>(mode < 0 ? 0 : mode > 7 ? 7 : mode)));
+    return static_cast<int>(srpc_impl::g_sx_mode.exchange(static_cast<uint32_t>(mode < 0 ? 0 : mode > 15 ? 15 : mode)));
 }

@@ -17,9 +17,12 @@ Tests taking the `path` fixture run once per table mode of the decoder
 (sdx.hip; the srpc_debug_stream_tables test hook): "tables" as the library
 runs it (every block's table holds the chains from every plausible position
 of its first 64 bytes); "primary" tables holding only each block's first
-speculated start (every other entry is found in no table and walked from
-global memory by the scan); "walk" empty tables (every block the cursor
-enters is walked).  Every mode meets the same cases.
+speculated start and "walk" empty tables -- in both the first scan meets
+positions no table holds, and the repair pass (round 6) gives every block
+the exits of the block before as slots; "walk_norepair" empty tables and no
+repair pass (every block the cursor enters is walked, the round-5 path, kept
+as the fallback of a block whose exit slots overflow).  Every mode meets the
+same cases.
 """
 import ctypes
 import json
@@ -41,10 +44,10 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
 from tests.streams import straddler_stream as _straddler_stream  # noqa: E402
 from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty, host, read_status, status_buf  # noqa: E402
 
-RES_OFF, RES_MISS = 1, 2  # srpc_unpack_status.reserved bits (srpc_gpu.h)
+RES_OFF, RES_MISS, RES_REPAIR = 1, 2, 4  # srpc_unpack_status.reserved bits (srpc_gpu.h)
 
 
-MODES = {"tables": 0, "primary": 1, "walk": 2}
+MODES = {"tables": 0, "primary": 1, "walk": 2, "walk_norepair": 2 | 8}
 
 
 @pytest.fixture(params=list(MODES))
@@ -160,6 +163,8 @@ def test_random_streams(n, schema, maxlen, envelope, path):
         # that walked a block from global memory: bits 8-31)
         assert r >> 8 <= 1 + blocks // 20, (r >> 8, blocks)
     if path == "walk" and blocks > 64:
+        assert r & RES_REPAIR, r
+    if path == "walk_norepair" and blocks > 64:
         assert r & RES_MISS and r >> 8 >= 1, r
 
 
@@ -290,8 +295,8 @@ def test_adversarial_streams_at_scale(n, schema, path):
     zero-heavy strings (int8, string, int16, string), and records of zeros
     only (multiple_primitives with empty strings: every one of its 18 phases
     parses, to the end of the stream).  Checked against the oracle's cursor."""
-    if path != "tables" and n >= 1 << 22:
-        pytest.skip("tables with no slots walk every block from global memory: covered at 1M")
+    if path == "walk_norepair" and n >= 1 << 22:
+        pytest.skip("no repair: every block walked from global memory: covered at 1M")
     rng = np.random.default_rng(n + len(schema))
     if schema == "zh4":
         kinds = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
@@ -326,8 +331,10 @@ def test_long_zero_strings_entries_no_block_guesses(n, path):
     r = stream_unpack.last_reserved
     if path == "tables":
         assert r >> 8 == 0, r  # no block walked
-    elif n >= 3000:
+    elif path == "walk_norepair" and n >= 3000:
         assert r & RES_MISS and r >> 8 > 0, r
+    elif n >= 3000:
+        assert r & RES_REPAIR and r >> 8 == 0, r  # every entry an exit slot: nothing walked
 
 
 ZH4 = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
@@ -338,17 +345,21 @@ ZH4 = [oracle.INT8, oracle.STRING, oracle.INT16, oracle.STRING]
     (1 << 22, (1, 960), (65, 1000), "zero"),    # the verdict's stream at 4M records
     (1 << 20, (1, 6000), (65, 6000), "zero"),   # straddlers of up to 12 KiB
     (1 << 16, (1, 960), (65, 1000), "zero"),
-    (1 << 16, (1, 900), (65, 100), "heavy")])   # zero-heavy straddlers: the residual (walked)
+    (1 << 16, (1, 900), (65, 100), "heavy"),    # zero-heavy straddlers starting within 1 KiB: landing slots
+    (1 << 18, (1, 6000), (65, 100), "heavy"),   # ... up to 6000 B before the edge: the repair pass (round 6)
+    (1 << 20, (1, 6000), (65, 6000), "heavy")])
 def test_straddling_records_at_every_block(n, lead, over, fill, path):
     """a record straddles EVERY 8 KiB boundary and
     ends past the block's window, where no speculated start is.  Records of
     zero bytes (the verdict's stream), whatever their length, are found by
     the zero-run rule -- nothing is walked in the library's tables mode
-    (reserved >> 8 == 0).  Straddlers with zero-heavy chars are the residual
-    case: their blocks are walked, serially.  Exact in every
-    mode."""
-    if path != "tables" and n > 1 << 16:
-        pytest.skip("tables with no slots walk every block: covered at 64K records")
+    (reserved >> 8 == 0).  Zero-heavy straddlers that start within 1 KiB of
+    the edge end at landing slots; longer ones (57.9
+    ms for 256K records, one block after another walked by one wave) send
+    the call through the repair pass: every block's entry is then an exit
+    slot, nothing is walked.  Exact in every mode."""
+    if path == "walk_norepair" and n > 1 << 16:
+        pytest.skip("no repair: every block walked, serially: covered at 64K records")
     rng = np.random.default_rng(n + lead[1] + over[1] + len(fill))
     cols, offs = _straddler_stream(n, rng, lead, over, fill)
     p = GpuPacker(Schema("Z", tuple((f"f{i}", k) for i, k in enumerate(ZH4))))
@@ -356,10 +367,12 @@ def test_straddling_records_at_every_block(n, lead, over, fill, path):
     rec = check_clean(p, ZH4, wire, n)
     assert np.array_equal(rec, _rec_offsets(ZH4, offs, n))
     r = stream_unpack.last_reserved
-    if path == "tables" and fill == "zero":
-        assert r >> 8 == 0, (r >> 8, len(wire) // 8192)
-    elif path != "tables" and len(wire) > 64 * 8192:
+    if path == "tables" and (fill == "zero" or lead[1] < 1024):
+        assert r >> 8 == 0 and not r & RES_REPAIR, (r >> 8, len(wire) // 8192)
+    elif path == "walk_norepair" and len(wire) > 64 * 8192:
         assert r & RES_MISS, r
+    elif path != "walk_norepair":  # the repair pass ran where it had to, and nothing was walked
+        assert r >> 8 == 0, (r, len(wire) // 8192)
 
 
 def test_records_across_block_edges_and_margin(path):

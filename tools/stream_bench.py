@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--tables", type=int, default=0,
                     help="srpc_debug_stream_tables bits (sdx.hip): 1 sF-only tables, 2 empty tables, "
-                         "4 the exact speculation filter")
+                         "4 the exact speculation filter, 8 no repair pass")
     args = ap.parse_args()
 
     import numpy as np
@@ -153,11 +153,12 @@ def main():
         alg = W + col_bytes + str_bytes + 8 * (n + 1) * nstr + 8 * (n + 1)
         row = {"case": name, "records": n, "wire_bytes": W, "alg_bytes": alg, "us": round(t * 1e6, 2),
                "GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 8e12, 4), "parity_ok": bool(ok),
-               "blocks": (W + 8191) // 8192, "walk_waves": reserved >> 8, "diag_bits": reserved & 3,
-               "off_primary": bool(reserved & 1), "walked_miss": bool(reserved & 2)}
+               "blocks": (W + 8191) // 8192, "walk_waves": reserved >> 8, "diag_bits": reserved & 7,
+               "off_primary": bool(reserved & 1), "walked_miss": bool(reserved & 2), "repaired": bool(reserved & 4)}
         rows.append(row)
         print(f'{name:36s} {n:9d} rec {W / 2**20:8.1f} MiB  {row["us"]:9.1f} us  {row["GBps"]:7.1f} GB/s '
               f'({row["frac"]:.3f})  parity={ok}  off_primary={row["off_primary"]} walked={row["walked_miss"]} '
+              f'repaired={row["repaired"]} '
               f'walk_waves {row["walk_waves"]}/{row["blocks"]} blocks',
               flush=True)
 
@@ -186,6 +187,10 @@ def main():
     # the residual: zero-heavy straddlers that start more than kPre before the boundary
     case("zh4_straddle_heavy_long_256K", zh, 1 << 18,
          lambda k, n, r: straddler_stream(n, r, (1100, 4000), (65, 1000), "heavy"))
+    # (its random counterpart: the same schema and record count)
+    case("zh4_random_256K", zh, 1 << 18, lambda k, n, r: gen_random(k, n, r, 24))
+    case("zh4_straddle_heavy_long_4M", zh, 1 << 22,
+         lambda k, n, r: straddler_stream(n, r, (1100, 6000), (65, 6000), "heavy"))
     if args.out:
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:
