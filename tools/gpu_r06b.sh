@@ -9,4 +9,7 @@ timeout -k 10 300 python3 -u tools/stream_bench.py --reps 5 --only 256K >> gpuru
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --ignore=tests/test_gpu_stream.py > gpurun_out/pytest_gpu_r06b.log 2>&1 || exit 4
 timeout -k 10 300 python3 bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 --records 4194304 > gpurun_out/bench_spawn_gloo2.log 2>&1 || exit 5
 timeout -k 10 120 python3 bench.py --gpus 2 --steps 5 > gpurun_out/bench_nccl2_refused.log 2>&1; echo "nccl2 rc=$?" >> gpurun_out/bench_nccl2_refused.log
+
+# interleaved A/B: landing slots kept (cur) / dropped (noland, the repair pass covers them) / round 5
+bash tools/ab_variants.sh "cur noland r05" "string_0-16_8M multiple_primitives_str0-64 zh4_random_4M zh4_straddle_heavy_4M zh4_straddle_heavy_long_256K zh4_random_256K" 2 5 > gpurun_out/ab_noland_r06b.log 2>&1 || exit 6
 exit 0
