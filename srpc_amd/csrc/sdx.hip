@@ -623,13 +623,71 @@ struct Chunks : ChunkChars<NC> {
     uint64_t ws[kBlock / 64];
 };
 
+// The zero map of a zero-heavy block (round 6; built only where k_sx_spec
+// repaired the speculation, header word 2 bit 17): bit j = bytes [b0 + 32 j,
+// b0 + 32 j + 32) hold a nonzero byte or lie past the stage.  A chain that
+// meets a run of zero bytes off the speculation crosses it in one step: with
+// no prefix, a record of Z = fixed_bytes zero bytes (every string empty)
+// parses at every position of the run, so from q the next k = (run end - q) / Z
+// records are zero records (no chars) -- the round-5 walk parsed them one by
+// one (all-zero multiple_primitives 6.5x its random row).  Random blocks never
+// build or read it: their chains take walk_chain<..., ZM = false>.
+constexpr uint32_t kZC = (kSB + kMargin) / 32;  // chunks the map covers
+constexpr uint32_t kZW = (kZC + 63) / 64;       // its words
+// Every thread of the workgroup takes part; a barrier at the end.
+__device__ __forceinline__ void build_zmap(const StagedRd& rd, uint64_t b0, uint64_t* zm) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t j0 = tid & ~63u; j0 < kZW * 64; j0 += kBlock) {
+        const uint32_t j = j0 + lane;
+        const uint64_t lo = b0 + 32ull * j;
+        bool nz = true;
+        if (j < kZC && lo >= rd.lo && lo + 32 <= rd.hi) {
+            lds_u32c* q = reinterpret_cast<lds_u32c*>(rd.lds + (lo - rd.base));  // (b0 - base: a multiple of 16)
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v |= q[k];
+            nz = v != 0;
+        }
+        const uint64_t m = __ballot(nz);
+        if (lane == 0) zm[j0 >> 6] = m;
+    }
+    __syncthreads();
+}
+// The first nonzero byte at or after q (q >= b0), or the end of what the map
+// covers: bytes [q, result) are zero.
+template <class Rd>
+__device__ __forceinline__ uint64_t zero_run_end(const Rd& rd, const uint64_t* zm, uint64_t b0, uint64_t q) {
+    uint32_t j = static_cast<uint32_t>((q - b0) >> 5);
+    if (j >= kZC) return q;
+    if ((zm[j >> 6] >> (j & 63)) & 1) {  // q's chunk: byte by byte to its end
+        const uint64_t ce = b0 + 32ull * (j + 1);
+        for (uint64_t p = q; p < ce; ++p)
+            if (rd.u8(p)) return p;
+        ++j;
+    }
+    // the next chunk with a nonzero byte
+    for (; j < kZC; j = (j | 63) + 1) {
+        const uint64_t w = zm[j >> 6] >> (j & 63);
+        if (w) {
+            j += __builtin_ctzll(w);
+            break;
+        }
+    }
+    if (j >= kZC) return b0 + 32ull * kZC;
+    const uint64_t cl = b0 + 32ull * j;
+    for (uint64_t p = cl; p < cl + 32; ++p)
+        if (rd.u8(p)) return p;
+    return cl + 32;
+}
+
 // The chain from x (x >= the block start): explicit records are parsed until
 // the walk meets a speculated chunk start, whose segment is then taken whole
 // from the scans (O(1)), and so on.  REC: the explicit starts go to xl (u16
 // offsets from the block, ascending) and jumped chunks to the jump mask.
-template <int NC, bool REC, class Rd>
+// ZM: runs of zero bytes crossed in one step (the zero map zm, above).
+template <int NC, bool REC, bool ZM = false, class Rd>
 __device__ St<NC> walk_chain(const SxArgs& a, const Rd& rd, Chunks<NC>& L, uint64_t b0, uint64_t b1, uint64_t x,
-                             uint16_t* xl, uint32_t* nx) {
+                             uint16_t* xl, uint32_t* nx, const uint64_t* zm = nullptr) {
     St<NC> g{};
     uint64_t q = x;
     uint32_t ne = 0;
@@ -654,6 +712,23 @@ __device__ St<NC> walk_chain(const SxArgs& a, const Rd& rd, Chunks<NC>& L, uint6
                 break;
             }
             continue;
+        }
+        if constexpr (ZM) {
+            const uint32_t Z = a.fixed_bytes;
+            if (!a.prefix_len) {
+                const uint64_t re = zero_run_end(rd, zm, b0, q);
+                if (re >= q + Z && re <= a.W) {
+                    // records q, q + Z, ... while they lie in the run, the last one
+                    // the first to start at or past b1 at most
+                    const uint64_t k = min<uint64_t>((re - q) / Z, (b1 - q + Z - 1) / Z);
+                    if (REC)
+                        for (uint64_t i = 0; i < k; ++i) xl[ne + i] = static_cast<uint16_t>(q + i * Z - b0);
+                    ne += static_cast<uint32_t>(k);
+                    g.cnt += k;
+                    q += k * Z;
+                    continue;
+                }
+            }
         }
         uint32_t err;
         const uint64_t q2 = parse_rd<NC>(a, rd, q, &err, g.ch);
@@ -1038,6 +1113,7 @@ struct SpecLds {
     // part (the record list written out) holds the landing slots
     alignas(4) uint8_t list[kBlock * kListCap];
     uint32_t s_nx;  // landings found (wave 1's counter)
+    uint64_t zm[kZW];  // the zero map (zero-heavy blocks only)
 };
 static_assert(64 * kListCap >= 2 * kX, "the landing slots fit wave 0's part of the chunk lists");
 
@@ -1046,7 +1122,7 @@ static_assert(64 * kListCap >= 2 * kX, "the landing slots fit wave 0's part of t
 template <int NC>
 __device__ __forceinline__ void land_slots(const SxArgs& a, const StagedRd& rd, const StageOnlyRd& so,
                                            const SxScratch& S, SpecLds<NC>& L, Chunks<NC>& C, uint64_t b,
-                                           uint64_t b0, uint64_t b1, uint64_t sF2) {
+                                           uint64_t b0, uint64_t b1, uint64_t sF2, bool zflag) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t W = a.W;
     // The zero run the window ends in (find_slot's zero-run rule, for schemas
@@ -1190,7 +1266,8 @@ __device__ __forceinline__ void land_slots(const SxArgs& a, const StagedRd& rd, 
     for (uint32_t j = lane; j < nx; j += 64) {
         const uint32_t o = xl[j];
         st_store<NC>(S.ent + (b * kEnt + kWin + 1 + j) * ew<NC>(),
-                     walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
+                     zflag ? walk_chain<NC, false, true>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr, L.zm)
+                           : walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
         S.xp[b * kX + j] = static_cast<uint16_t>(o);
     }
     if (lane == 0)
@@ -1383,6 +1460,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
     // of record by record (here and in k_sx_decode, which walks its chunks
     // from the repaired starts).  A first pass that joins fewer than 4
     // segments ends the repair.  Random blocks have 1-4 segments: not taken.
+    bool zflag = false;  // a zero-heavy block: its chains cross zero runs by the zero map
     {
         uint32_t ntail = 0;
 #pragma unroll
@@ -1391,6 +1469,10 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
         if (false) {  // (A/B)
 #else
         if (__builtin_expect(ntail > kRepairMin, 0)) {
+#endif
+#ifndef SRPC_SX_NOZMAP
+            zflag = !a.prefix_len && NC < 3;  // (four string fields: the walker's registers spill)
+            if (zflag) build_zmap(rd, b0, L.zm);
 #endif
 #pragma nounroll
             for (uint32_t pass = 0; pass < kRepairMax; ++pass) {
@@ -1462,13 +1544,14 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
         if (tid == kBlock - 1) {
             if (sF2 != ~0ull)
                 st_store<NC>(S.ent + (b * kEnt + kWin) * ew<NC>(),
-                             walk_chain<NC, false>(a, rd, C, b0, b1, sF2, nullptr, nullptr));
+                             zflag ? walk_chain<NC, false, true>(a, rd, C, b0, b1, sF2, nullptr, nullptr, L.zm)
+                                   : walk_chain<NC, false>(a, rd, C, b0, b1, sF2, nullptr, nullptr));
             S.hdr[kHdr * b + 3] = sF2;
         }
         return;
     }
     if (tid >= 64) {
-        land_slots<NC>(a, rd, so, S, L, C, b, b0, b1, sF2);
+        land_slots<NC>(a, rd, so, S, L, C, b, b0, b1, sF2, zflag);
         return;
     }
     const uint32_t F = next_bit(C.has, 0);
@@ -1498,7 +1581,8 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
     }
     St<NC> mine{};
     if (mycand != ~0ull) {
-        mine = walk_chain<NC, false>(a, rd, C, b0, b1, mycand, nullptr, nullptr);
+        mine = zflag ? walk_chain<NC, false, true>(a, rd, C, b0, b1, mycand, nullptr, nullptr, L.zm)
+                     : walk_chain<NC, false>(a, rd, C, b0, b1, mycand, nullptr, nullptr);
         const uint32_t k = __builtin_popcountll(vmask & ((1ull << lane) - 1));
         st_store<NC>(S.ent + (b * kEnt + k) * ew<NC>(), mine);
     }
@@ -1516,7 +1600,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
         uint64_t* h = S.hdr + kHdr * b;
         h[0] = wmask;
         h[1] = sF;
-        h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull) |
+        h[2] = nslots | (static_cast<uint64_t>(prim) << 8) | (one ? 1ull << 16 : 0ull) | (zflag ? 1ull << 17 : 0ull) |
                (static_cast<uint64_t>(min<uint32_t>(C.pcnt[kBlock], kMaxRec)) << 32);
         h[5] = 0;  // no exit slots (until a repair pass)
     }
@@ -2235,6 +2319,7 @@ struct DecLds {
     } u;
     alignas(8) uint16_t tbl[kMaxRec + 4];  // the block's records in order: offset from the block
     uint64_t ws[kBlock / 64];
+    uint64_t zm[kZW];  // the zero map (zero-heavy blocks only)
     uint32_t s_nexp;
 };
 
@@ -2313,9 +2398,12 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
     // the chain from the block's entry: explicit starts (xl, until the table is
     // built) and the chunks it jumped
     uint16_t* xl = L.u.w.xl;
+    const bool zf = (hmeta >> 17) & 1;  // a zero-heavy block (k_sx_spec built its zero map too)
+    if (zf) build_zmap(rd, b0, L.zm);
     if (tid == 0) {
         uint32_t ne = 0;
-        (void)walk_chain<0, true>(a, rd, C, b0, b1, x, xl, &ne);
+        if (zf) (void)walk_chain<0, true, true>(a, rd, C, b0, b1, x, xl, &ne, L.zm);
+        else (void)walk_chain<0, true>(a, rd, C, b0, b1, x, xl, &ne);
         L.s_nexp = ne;
     }
     __syncthreads();

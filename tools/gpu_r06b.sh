@@ -11,5 +11,5 @@ timeout -k 10 300 python3 bench.py --gpus 2 --dist-backend gloo --steps 10 --war
 timeout -k 10 120 python3 bench.py --gpus 2 --steps 5 > gpurun_out/bench_nccl2_refused.log 2>&1; echo "nccl2 rc=$?" >> gpurun_out/bench_nccl2_refused.log
 
 # interleaved A/B: landing slots kept (cur) / dropped (noland, the repair pass covers them) / round 5
-bash tools/ab_variants.sh "cur noland r05" "string_0-16_8M multiple_primitives_str0-64 zh4_random_4M zh4_straddle_heavy_4M zh4_straddle_heavy_long_256K zh4_random_256K" 2 5 > gpurun_out/ab_noland_r06b.log 2>&1 || exit 6
+bash tools/ab_variants.sh "r05 cur zm zmnl" "string_0-16_8M multiple_primitives_str0-64 zh4_random_4M multiple_primitives_zeros_4M zh4_straddle_heavy_4M zh4_straddle_heavy_long_256K zh4_random_256K" 1 5 > gpurun_out/ab_noland_r06b.log 2>&1 || exit 6
 exit 0
