@@ -133,20 +133,29 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* t
 }
 
 // Every scan kernel takes `gate`: when non-null and *gate == 0 it does nothing
-// (the single-string unpack's error path, see k_unpack_var_walk).
+// (the single-string unpack's error path, see k_unpack_var_walk).  The reduce
+// and apply kernels take scan block bx = blockIdx.x, blockIdx.x + gridDim.x,
+// ... of nb: a gated scan is launched with a bounded grid, so on the (usual)
+// exact batch its two no-op launches dispatch at most kGatedGrid workgroups
+// instead of one per 2048 records (3.8 us each at 8M records,
+// profiles/r04_short_string_unpack_kernels.csv).
+constexpr uint32_t kGatedGrid = 512;
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_t* partial, const uint32_t* gate) {
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(F f, uint64_t n, uint64_t* partial, const uint32_t* gate,
+                                                        uint64_t nb) {
     if (gate && *gate == 0) return;
-    const uint64_t base = blockIdx.x * kScanBlock;
-    uint64_t s = 0;
+    for (uint64_t bx = blockIdx.x; bx < nb; bx += gridDim.x) {
+        const uint64_t base = bx * kScanBlock;
+        uint64_t s = 0;
 #pragma unroll
-    for (int j = 0; j < kScanItems; ++j) {
-        const uint64_t i = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
-        if (i < n) s += f(i);
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint64_t i = base + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+            if (i < n) s += f(i);
+        }
+        uint64_t tot;
+        (void)block_exclusive_scan(s, &tot);
+        if (threadIdx.x == 0) partial[blockIdx.y * (nb + 1) + bx] = tot;
     }
-    uint64_t tot;
-    (void)block_exclusive_scan(s, &tot);
-    if (threadIdx.x == 0) partial[blockIdx.y * (gridDim.x + 1ull) + blockIdx.x] = tot;
 }
 
 // One workgroup: exclusive scan of nb partials in place, partial[nb] = total.
@@ -182,7 +191,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
     out = scan_out(f, out);
     if (tile_first) tile_first += blockIdx.y * max_tiles * meta_stride;
     __shared__ uint64_t v[kScanBlock];
-    const uint64_t base = blockIdx.x * kScanBlock;
+    for (uint64_t bx = blockIdx.x; bx < nb; bx += gridDim.x) {
+    const uint64_t base = bx * kScanBlock;
 #pragma unroll
     for (int j = 0; j < kScanItems; ++j) {  // coalesced reads, staged in LDS
         const uint32_t k = j * kBlock + threadIdx.x;
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
         s += v[threadIdx.x * kScanItems + j];
     }
     uint64_t tot;
-    const uint64_t pre = block_exclusive_scan(s, &tot) + partial[blockIdx.x];
+    const uint64_t pre = block_exclusive_scan(s, &tot) + partial[bx];
 #pragma unroll
     for (int j = 0; j < kScanItems; ++j) {
         const uint32_t k = threadIdx.x * kScanItems + j;
@@ -213,7 +223,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(F f, M meta, uint64_t n, 
         const uint32_t k = j * kBlock + threadIdx.x;
         if (base + k < n) out[base + k] = v[k];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = partial[nb];
+    if (bx == 0 && threadIdx.x == 0) out[n] = partial[nb];
+    __syncthreads();  // (the next scan block overwrites v)
+    }
 }
 
 // ---- record / chunk location -------------------------------------------------
@@ -2216,9 +2228,10 @@ int launch_scan(F f, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* til
                 const uint32_t* gate = nullptr, uint32_t domains = 1) {
     const uint64_t nb = std::max<uint64_t>(1, scan_blocks(n));
     if (nb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-    launch(k_scan_reduce<F>, dim3(static_cast<uint32_t>(nb), domains), dim3(kBlock), 0, s, f, n, partial, gate);
+    const uint32_t gx = static_cast<uint32_t>(gate ? std::min<uint64_t>(nb, kGatedGrid) : nb);
+    launch(k_scan_reduce<F>, dim3(gx, domains), dim3(kBlock), 0, s, f, n, partial, gate, nb);
     launch(k_scan_partials, dim3(1, domains), dim3(kBlock), 0, s, partial, nb, gate);
-    launch(k_scan_apply<F, M>, dim3(static_cast<uint32_t>(nb), domains), dim3(kBlock), 0, s, f, M{}, n, partial, nb, out,
+    launch(k_scan_apply<F, M>, dim3(gx, domains), dim3(kBlock), 0, s, f, M{}, n, partial, nb, out,
            tile_first, max_tiles, tile_bytes, meta_stride, gate);
     return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
 }
