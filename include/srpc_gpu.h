@@ -96,6 +96,8 @@ typedef struct srpc_unpack_status {
                                    (that block was walked record by record),
                                    bit 2 = the first scan met such a position and
                                    the repair pass gave every block exit slots,
+                                   bit 3 = some block had more possible entries
+                                   than its exit slots hold (those may walk),
                                    bits 8-31 = scan waves that walked (saturating);
                                    0 from every other call                     */
     uint64_t first_bad_record;  /* smallest failing record index, or UINT64_MAX */

@@ -89,8 +89,8 @@ constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
 // every position of the block before (and from longer records of blocks
 // further back), so the cursor's entry into a block is always a slot -- see
 // k_sx_fan / k_sx_exits.
-constexpr uint32_t kE = 64;                      // exit slots per block
-constexpr uint32_t kNear = 128;                  // a block's live exits into the next block, at most
+constexpr uint32_t kE = 128;                     // exit slots per block
+constexpr uint32_t kNear = 256;                  // a block's live exits into the next block, at most
 constexpr uint32_t kFarIn = 64;                  // exits of longer records a block receives, at most
 constexpr uint32_t kFarSet = 256;                // k_sx_fan's set of a block's far exits (LDS hash)
 constexpr uint32_t kXS = kX + kE;                // a wave's LDS copy of a block's landing + exit slots
@@ -1752,12 +1752,10 @@ struct ExitLds {
     alignas(16) uint8_t pre[kMaxPrefix + 16];
     Chunks<NC> c;
     uint16_t xs[kXS];                 // the block's landing slots, then (kX on) its exit slots
-    uint16_t cand[kNear + kFarIn];
-    uint16_t keep[kNear + kFarIn];
-    uint8_t first[kNear + kFarIn];
-    uint32_t nkeep;
+    uint32_t keep[kSB / 32];          // the candidates its table does not hold (a bit per position)
+    uint64_t ws[kBlock / 64];
+    uint64_t zm[kZW];
 };
-static_assert(kNear + kFarIn <= kBlock, "a thread per candidate");
 
 // Block c's exit slots: the live exits of block c - 1's chains into it and of
 // longer records' into it (k_sx_fan), minus the positions its table already
@@ -1773,8 +1771,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __
         const uint32_t nn = min<uint32_t>(xn & 0xffff, kNear), nf = min<uint32_t>(fin, kFarIn), nc = nn + nf;
         if (nc == 0) continue;  // (uniform: every thread read the same words)
         const uint64_t b0 = c * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
-        if (tid < nc) L.cand[tid] = tid < nn ? S.xnear[(c - 1) * kNear + tid] : S.xin[c * kFarIn + (tid - nn)];
-        if (tid == 0) L.nkeep = 0;
+        L.keep[tid] = 0;
         const uint64_t* h = S.hdr + kHdr * c;
         const uint64_t h0 = h[0], h1 = h[1], h3 = h[3], h4 = h[4];
         const uint32_t meta = static_cast<uint32_t>(h[2]), nx = nx_used(a, h4);
@@ -1796,38 +1793,34 @@ __global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __
         if (lane == 0) C.has[tid >> 6] = hm;
         __syncthreads();
         link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);  // (ends in a barrier)
-        // the candidates the table does not hold yet
-        if (tid < nc) {
-            const uint32_t o = L.cand[tid];
-            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0) {
-                const uint32_t k = atomicAdd(&L.nkeep, 1u);
-                L.keep[k] = static_cast<uint16_t>(o);
-            }
+        // the candidates the table does not hold yet, deduplicated (a near exit
+        // can also arrive as a far one) and sorted by a bitmap
+        for (uint32_t i = tid; i < nc; i += kBlock) {
+            const uint32_t o = i < nn ? S.xnear[(c - 1) * kNear + i] : S.xin[c * kFarIn + (i - nn)];
+            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0)
+                atomicOr(&L.keep[o >> 5], 1u << (o & 31));
         }
         __syncthreads();
-        const uint32_t nk = L.nkeep;
-        // sorted, duplicates dropped (a near exit can also arrive as a far one)
-        uint32_t mine = 0;
-        if (tid < nk) {
-            mine = L.keep[tid];
-            bool first = true;
-            for (uint32_t k = 0; k < tid; ++k) first &= L.keep[k] != mine;
-            L.first[tid] = first ? 1 : 0;
+        uint32_t m = L.keep[tid];
+        uint64_t tot;
+        uint64_t k = block_xscan(__builtin_popcount(m), &tot, L.ws);
+        while (m) {
+            const uint32_t bit = __builtin_ctz(m);
+            m &= m - 1;
+            if (k < kE) L.xs[kX + k] = static_cast<uint16_t>(32 * tid + bit);
+            ++k;
         }
+        const uint32_t ne = static_cast<uint32_t>(min<uint64_t>(tot, 0xffff));
         __syncthreads();
-        uint32_t ne = 0;
-        if (tid < nk && L.first[tid]) {
-            uint32_t rank = 0;
-            for (uint32_t k = 0; k < nk; ++k) rank += L.first[k] && L.keep[k] < mine;
-            if (rank < kE) L.xs[kX + rank] = static_cast<uint16_t>(mine);
-        }
-        ne = static_cast<uint32_t>(__syncthreads_count(tid < nk && L.first[tid]));
         const uint32_t nu = min(ne, kE);
-        for (uint32_t k = tid; k < nu; k += kBlock) {
-            const uint32_t o = L.xs[kX + k];
-            st_store<NC>(S.ent + (c * kEnt + kWin + 1 + kX + k) * ew<NC>(),
-                         walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
-            S.ep[c * kE + k] = static_cast<uint16_t>(o);
+        const bool zf = ((meta >> 17) & 1) && NC < 3;  // a zero-heavy block: chains cross zero runs by its zero map
+        if (zf) build_zmap(rd, b0, L.zm);
+        for (uint32_t j = tid; j < nu; j += kBlock) {
+            const uint32_t o = L.xs[kX + j];
+            st_store<NC>(S.ent + (c * kEnt + kWin + 1 + kX + j) * ew<NC>(),
+                         zf ? walk_chain<NC, false, true>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr, L.zm)
+                            : walk_chain<NC, false>(a, rd, C, b0, b1, b0 + o, nullptr, nullptr));
+            S.ep[c * kE + j] = static_cast<uint16_t>(o);
         }
         if (tid == 0) {
             const bool over = ne > kE || (xn >> 16) || fin > kFarIn;
@@ -2343,8 +2336,8 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
         }
     }
     if (b == 0 && tid == 0 && st && kDecode) {  // diagnostics (srpc_unpack_status.reserved)
-        const uint64_t miss = S.ctl[kCtlMiss], off = S.ctl[kCtlOff], rep = S.ctl[kCtlRepair];
-        st->reserved = (off ? 1u : 0u) | (miss ? 2u : 0u) | (rep ? 4u : 0u) |
+        const uint64_t miss = S.ctl[kCtlMiss], off = S.ctl[kCtlOff], rep = S.ctl[kCtlRepair], ov = S.ctl[kCtlOver];
+        st->reserved = (off ? 1u : 0u) | (miss ? 2u : 0u) | (rep ? 4u : 0u) | (ov ? 8u : 0u) |
                        (static_cast<uint32_t>(min<uint64_t>(miss, 0xffffff)) << 8);
     }
     if (b >= a.nb) return;

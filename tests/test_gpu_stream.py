@@ -44,7 +44,7 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
 from tests.streams import straddler_stream as _straddler_stream  # noqa: E402
 from tests.test_gpu_parity import _random_string_batch, _rec_offsets, dev, empty, host, read_status, status_buf  # noqa: E402
 
-RES_OFF, RES_MISS, RES_REPAIR = 1, 2, 4  # srpc_unpack_status.reserved bits (srpc_gpu.h)
+RES_OFF, RES_MISS, RES_REPAIR, RES_OVER = 1, 2, 4, 8  # srpc_unpack_status.reserved bits (srpc_gpu.h)
 
 
 MODES = {"tables": 0, "primary": 1, "walk": 2, "walk_norepair": 2 | 8}

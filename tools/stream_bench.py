@@ -153,12 +153,12 @@ def main():
         alg = W + col_bytes + str_bytes + 8 * (n + 1) * nstr + 8 * (n + 1)
         row = {"case": name, "records": n, "wire_bytes": W, "alg_bytes": alg, "us": round(t * 1e6, 2),
                "GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 8e12, 4), "parity_ok": bool(ok),
-               "blocks": (W + 8191) // 8192, "walk_waves": reserved >> 8, "diag_bits": reserved & 7,
-               "off_primary": bool(reserved & 1), "walked_miss": bool(reserved & 2), "repaired": bool(reserved & 4)}
+               "blocks": (W + 8191) // 8192, "walk_waves": reserved >> 8, "diag_bits": reserved & 15,
+               "off_primary": bool(reserved & 1), "walked_miss": bool(reserved & 2), "repaired": bool(reserved & 4), "exit_overflow": bool(reserved & 8)}
         rows.append(row)
         print(f'{name:36s} {n:9d} rec {W / 2**20:8.1f} MiB  {row["us"]:9.1f} us  {row["GBps"]:7.1f} GB/s '
               f'({row["frac"]:.3f})  parity={ok}  off_primary={row["off_primary"]} walked={row["walked_miss"]} '
-              f'repaired={row["repaired"]} '
+              f'repaired={row["repaired"]} overflow={row["exit_overflow"]} '
               f'walk_waves {row["walk_waves"]}/{row["blocks"]} blocks',
               flush=True)
 
