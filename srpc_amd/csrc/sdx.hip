@@ -123,6 +123,7 @@ constexpr uint32_t kCtlT = 3;        // ... from record T
 constexpr uint32_t kCtlTot = 4;      // ... str_offs value per string ordinal (kMaxNC + 1 words)
 constexpr uint32_t kCtlRepair = 8;   // the first scan met a position no table holds: repair, scan again
 constexpr uint32_t kCtlOver = 9;     // blocks whose exit slots overflowed (diagnostics)
+constexpr uint32_t kCtlDone = 10;    // k_sx_groups workgroups done, per pass (2 words): the last runs the scan
 constexpr uint32_t kCtlWords = 16;
 
 // stop bits: bit 0 = the chain stopped, bits 1-2 = why (SRPC_STATUS_PREFIX / _BOUNDS)
@@ -1980,14 +1981,12 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
 // block, and the cursor enters a group there rarely: k_sx_top then takes
 // that group block by block).  Test-hook mode 8 (no repair): pass 0 walks the
 // primary chains, as pass 1 does.
+// One wave: group g's table (k_sx_groups).
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
-                                                      uint32_t pass) {
-    if (pass && !S.ctl[kCtlRepair]) return;  // (the second scan runs only after a repair)
+__device__ void sx_group(const SxArgs& a, const uint8_t* __restrict__ w, const SxScratch& S, uint32_t pass,
+                         uint64_t g, uint8_t* stage, Chunks<NC>& mch, uint16_t* xs) {
     const bool walk_prim = pass || (a.mode & 8);
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-    if (g >= a.ng) return;
     const uint64_t bf = g * kGroup;
     const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
     Held<NC> hv;
@@ -1997,11 +1996,6 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     const bool has3 = rl64(hv.h3, 0) != ~0ull;
     const uint32_t nx0 = nx_used(a, rl64(hv.h4, 0)), ne0 = h5_ne(rl64(hv.h5, 0));
     const uint32_t total = ns0 + (has3 ? 1 : 0) + nx0 + ne0;
-    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
-    __shared__ uint16_t xss[kBlock / 64][kXS];
-    uint8_t* stage = stages[threadIdx.x >> 6];
-    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
-    uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     uint64_t* q = S.gp + g * (kHdr + ew<NC>());
     for (uint32_t k0 = 0; k0 < total; k0 += 64) {
@@ -2024,8 +2018,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
             const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
             if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
             St<NC> t = s;
-            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs,
-                              primary && walk_prim);
+            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mch, xs, primary && walk_prim);
             if (act) s = t;
         }
         if (act) st_store<NC>(S.gent + (g * kEnt + idx) * ew<NC>(), s);
@@ -2051,18 +2044,16 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
 // chain given up there) it asks for the repair pass (ctl kCtlRepair) and
 // ends, writing nothing; pass 1 runs only after a repair and walks what is
 // still missing (a block whose exit slots overflowed).  Mode 8: pass 0 walks.
+// Run by one wave: the last workgroup of k_sx_groups to finish (its wave 0,
+// with that wave's LDS), or k_sx_top where there are no groups.
 template <int NC, bool kDecode>
-__global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
-                                               srpc_unpack_status* st, uint32_t pass) {
-    if (pass && !S.ctl[kCtlRepair]) return;
+__device__ void sx_top(const SxArgs& a, const uint8_t* __restrict__ w, const SxScratch& S, srpc_unpack_status* st,
+                       uint32_t pass, uint8_t* stage, Chunks<NC>& mch, uint16_t* xs) {
     const bool may_walk = pass || (a.mode & 8);
     constexpr uint32_t E = ew<NC>();
     constexpr uint32_t R = kHdr + E;  // words of a group's record in S.gp
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t W = a.W;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
-    __shared__ Chunks<NC> mch;  // walk_miss's chunks
-    __shared__ uint16_t xs[kXS];
     St<NC> s{};
     bool miss = false, off = false;
     // lane l: group base + l -- its first block's header and the group's
@@ -2234,6 +2225,39 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
             st->first_bad_record = T;
         }
     }
+}
+
+template <int NC, bool kDecode>
+__global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                                      srpc_unpack_status* st, uint32_t pass) {
+    if (pass && !S.ctl[kCtlRepair]) return;  // (the second scan runs only after a repair)
+    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    __shared__ uint16_t xss[kBlock / 64][kXS];
+    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
+    __shared__ uint32_t s_last;
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    if (g < a.ng) sx_group<NC>(a, w, S, pass, g, stages[threadIdx.x >> 6], mchs[threadIdx.x >> 6],
+                               xss[threadIdx.x >> 6]);
+    // the last workgroup to finish runs the in-order scan (no waiting: the
+    // others have ended; their tables are published by the fences)
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlDone + pass]), 1ull) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (threadIdx.x < 64) sx_top<NC, kDecode>(a, w, S, st, pass, stages[0], mchs[0], xss[0]);
+}
+
+template <int NC, bool kDecode>
+__global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                               srpc_unpack_status* st, uint32_t pass) {
+    if (pass && !S.ctl[kCtlRepair]) return;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaveStage + 16];
+    __shared__ Chunks<NC> mch;  // walk_miss's chunks
+    __shared__ uint16_t xs[kXS];
+    sx_top<NC, kDecode>(a, w, S, st, pass, stage, mch, xs);
 }
 
 // A wave per group: every block's entry state, from the group's.
@@ -2703,8 +2727,9 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
     if (a.nb) launch(k_sx_spec<NC>, dim3(a.nb), dim3(kBlock), 0, s, a, wire, S);
     else hipLaunchKernelGGL(k_zero_ctl, dim3(1), dim3(64), 0, s, S.ctl);
     const uint32_t gw = (a.ng + kBlock / 64 - 1) / (kBlock / 64);
-    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, 0u);
-    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
+    // the groups' tables, then (their last workgroup) the in-order scan
+    if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 0u);
+    else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
     // the repair pass and the second scan: each workgroup reads one control
     // word and ends unless the first scan asked for them (a bounded grid)
     if (a.nb > 1) {
@@ -2712,8 +2737,8 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
         launch(k_sx_fan<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
         launch(k_sx_exits<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
     }
-    if (a.ng) launch(k_sx_groups<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, 1u);
-    launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 1u);
+    if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 1u);
+    else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 1u);
     if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
     const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
     launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
