@@ -41,7 +41,6 @@ struct Pipe {
     hipStream_t in = nullptr, k = nullptr, out = nullptr;
     hipEvent_t start = nullptr;
     hipEvent_t fence[3] = {};    // an error's drain: the last work of each internal stream
-    hipEvent_t idle[3] = {};     // recorded on return to the pool: the pipe's streams are idle once all three fired
     hipStream_t caller = nullptr;  // the caller stream of the call that last used it
     std::vector<hipEvent_t> ev;  // 3 per ring slot: input copied, kernel done, output copied
 };
@@ -51,8 +50,8 @@ struct Pipe {
 // call's bytes for milliseconds.  So a call takes, in order:
 // a free pipe last used with its own caller stream (its work is ordered
 // behind that stream's earlier calls anyway: nothing is serialised that was
-// not already), else a free pipe whose streams are idle (its `idle` events
-// have fired), else a new pipe.  Calls on different caller streams therefore
+// not already), else a free pipe whose streams are idle (hipStreamQuery of
+// each), else a new pipe.  Calls on different caller streams therefore
 // never queue their copies behind each other on shared internal streams while
 // the other's are in flight; the pool grows to the number of calls in flight
 // at once, not with the threads that made them, and a thread that exits
@@ -75,24 +74,23 @@ Pipe* make_pipe() {
               hipStreamCreateWithFlags(&p->out, fl) == hipSuccess &&
               hipEventCreateWithFlags(&p->start, hipEventDisableTiming) == hipSuccess;
     for (auto& e : p->fence) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-    for (auto& e : p->idle) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (ok) return p;
     for (hipStream_t q : {p->in, p->k, p->out})
         if (q) (void)hipStreamDestroy(q);
-    for (hipEvent_t e : {p->start, p->fence[0], p->fence[1], p->fence[2], p->idle[0], p->idle[1], p->idle[2]})
+    for (hipEvent_t e : {p->start, p->fence[0], p->fence[1], p->fence[2]})
         if (e) (void)hipEventDestroy(e);
     delete p;
     (void)hipGetLastError();
     return nullptr;
 }
 
-// True when every piece of work last enqueued on the pipe's streams has run
-// (an event never recorded counts as fired).  A not-ready query leaves no
-// error behind for the call's final hipGetLastError.
+// True when every piece of work enqueued on the pipe's streams has run.  (Not
+// by events recorded at the pipe's return: with those, the reuse test saw a
+// new pipe made after a device synchronize, i.e. no idle pipe found.)  A
+// not-ready query leaves no error behind for the call's final hipGetLastError.
 bool pipe_idle(Pipe* p) {
-    for (hipEvent_t e : p->idle) {
-        const hipError_t q = hipEventQuery(e);
-        if (q == hipSuccess) continue;
+    for (hipStream_t q : {p->in, p->k, p->out}) {
+        if (hipStreamQuery(q) == hipSuccess) continue;
         (void)hipGetLastError();
         return false;
     }
@@ -139,9 +137,6 @@ struct Lease {
     }
     void release() {
         if (!p) return;
-        // the last work of each internal stream: the pipe is idle once these fire
-        hipStream_t q[3] = {p->in, p->k, p->out};
-        for (int i = 0; i < 3; ++i) (void)hipEventRecord(p->idle[i], q[i]);
         p->caller = caller;
         std::lock_guard<std::mutex> lk(pool().mu);
         pool().free[device].push_back(p);
