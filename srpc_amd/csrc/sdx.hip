@@ -654,16 +654,34 @@ __device__ __forceinline__ void build_zmap(const StagedRd& rd, uint64_t b0, uint
     }
     __syncthreads();
 }
+// A bit per byte of the 32 bytes at cl (a chunk of the map): the byte is
+// nonzero, or lies past the stage (8 aligned dword reads).
+template <class Rd>
+__device__ __forceinline__ uint32_t chunk_nz(const Rd& rd, uint64_t cl) {
+    if (cl < rd.lo || cl + 32 > rd.hi) return ~0u;
+    lds_u32c* q = reinterpret_cast<lds_u32c*>(rd.lds + (cl - rd.base));  // (16-aligned: b0 - base is)
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t d = q[k];
+        // 0x80 in each byte of d that is nonzero
+        const uint32_t h = (((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d) & 0x80808080u;
+        // bits 7, 15, 23, 31 -> bits 0..3 of this dword's nibble
+        const uint32_t nib = ((h >> 7) & 1u) | ((h >> 14) & 2u) | ((h >> 21) & 4u) | ((h >> 28) & 8u);
+        m |= nib << (4 * k);
+    }
+    return m;
+}
+
 // The first nonzero byte at or after q (q >= b0), or the end of what the map
 // covers: bytes [q, result) are zero.
 template <class Rd>
 __device__ __forceinline__ uint64_t zero_run_end(const Rd& rd, const uint64_t* zm, uint64_t b0, uint64_t q) {
     uint32_t j = static_cast<uint32_t>((q - b0) >> 5);
     if (j >= kZC) return q;
-    if ((zm[j >> 6] >> (j & 63)) & 1) {  // q's chunk: byte by byte to its end
-        const uint64_t ce = b0 + 32ull * (j + 1);
-        for (uint64_t p = q; p < ce; ++p)
-            if (rd.u8(p)) return p;
+    if ((zm[j >> 6] >> (j & 63)) & 1) {  // q's chunk: its nonzero bytes at or after q
+        const uint32_t m = chunk_nz(rd, b0 + 32ull * j) & (~0u << ((q - b0) & 31));
+        if (m) return b0 + 32ull * j + __builtin_ctz(m);
         ++j;
     }
     // the next chunk with a nonzero byte
@@ -675,10 +693,8 @@ __device__ __forceinline__ uint64_t zero_run_end(const Rd& rd, const uint64_t* z
         }
     }
     if (j >= kZC) return b0 + 32ull * kZC;
-    const uint64_t cl = b0 + 32ull * j;
-    for (uint64_t p = cl; p < cl + 32; ++p)
-        if (rd.u8(p)) return p;
-    return cl + 32;
+    const uint32_t m = chunk_nz(rd, b0 + 32ull * j);
+    return b0 + 32ull * j + (m ? __builtin_ctz(m) : 32);
 }
 
 // The chain from x (x >= the block start): explicit records are parsed until
@@ -1473,7 +1489,17 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
 #endif
 #ifndef SRPC_SX_NOZMAP
             zflag = !a.prefix_len && NC < 3;  // (four string fields: the walker's registers spill)
-            if (zflag) build_zmap(rd, b0, L.zm);
+            if (zflag) {
+                build_zmap(rd, b0, L.zm);
+                // worth it where zero runs are long: at least half the block's
+                // chunks all zero (zero-heavy chars with a nonzero byte every
+                // ~20 make one-record runs: there the map costs more than it
+                // saves)
+                uint32_t zc = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < kSB / 32 / 64; ++k) zc += 64 - __builtin_popcountll(L.zm[k]);
+                zflag = 2 * zc >= kSB / 32;
+            }
 #endif
 #pragma nounroll
             for (uint32_t pass = 0; pass < kRepairMax; ++pass) {
@@ -1695,22 +1721,33 @@ __global__ __launch_bounds__(kBlock) void k_sx_fan(SxArgs a, const uint8_t* __re
             }
             if (!__syncthreads_or(more)) break;
         }
-        // the distinct exits: the next block's in a bitmap, later ones in a set
+        // the distinct exits: the next block's in a bitmap, later ones in a set.
+        // Most positions share a few exits (chains converge): the lanes of a
+        // wave holding one value elect one of them, and a bit already set is
+        // not set again -- an atomic per position on the same LDS word
+        // serialised the whole block (~1 ms a block on zero-heavy bytes).
         for (uint32_t i = tid; i < kSB; i += kBlock) {
-            const uint32_t v = L.J[i];
-            if (v == kJStop || v < kSB) continue;
-            const uint64_t x = b0 + v;
-            if (x >= a.W) continue;  // the wire's end: no block to enter
-            if (x < b1 + kSB) {
-                atomicOr(&L.nearm[(x - b1) >> 5], 1u << ((x - b1) & 31));
-            } else {
-                uint32_t h = (v * 2654435761u) >> 24, k = 0;
-                for (; k < kFarSet; ++k) {
-                    const uint32_t old = atomicCAS(&L.far[h], 0u, v);
-                    if (old == 0u || old == v) break;
-                    h = (h + 1) & (kFarSet - 1);
+            const uint32_t v0 = L.J[i];
+            uint32_t v = v0 == kJStop || v0 < kSB || b0 + v0 >= a.W ? 0u : v0;  // 0: no exit to record
+            for (uint64_t act = __ballot(v != 0); act; act = __ballot(v != 0)) {
+                const uint32_t lv = __builtin_amdgcn_readlane(v, __builtin_ctzll(act));  // the lowest such lane's
+                const uint64_t mine = __ballot(v == lv);
+                if (v == lv && (threadIdx.x & 63) == static_cast<uint32_t>(__builtin_ctzll(mine))) {
+                    const uint64_t x = b0 + lv;
+                    if (x < b1 + kSB) {
+                        const uint32_t wi = static_cast<uint32_t>((x - b1) >> 5), bit = 1u << ((x - b1) & 31);
+                        if (!(L.nearm[wi] & bit)) atomicOr(&L.nearm[wi], bit);
+                    } else {
+                        uint32_t h = (lv * 2654435761u) >> 24, k = 0;
+                        for (; k < kFarSet; ++k) {
+                            const uint32_t old = atomicCAS(&L.far[h], 0u, lv);
+                            if (old == 0u || old == lv) break;
+                            h = (h + 1) & (kFarSet - 1);
+                        }
+                        if (k == kFarSet) L.far_over = 1;
+                    }
                 }
-                if (k == kFarSet) L.far_over = 1;
+                if (v == lv) v = 0;
             }
         }
         __syncthreads();
