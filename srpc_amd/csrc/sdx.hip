@@ -2018,10 +2018,26 @@ __device__ __forceinline__ void through_block(const SxArgs& a, const uint8_t* w,
 // block, and the cursor enters a group there rarely: k_sx_top then takes
 // that group block by block).  Test-hook mode 8 (no repair): pass 0 walks the
 // primary chains, as pass 1 does.
-// One wave: group g's table (k_sx_groups).
+// A wave's LDS for sx_group's shared continuations (below).
+template <int NC>
+struct GroupDedup {
+    uint64_t ux[64];             // distinct positions the group's chains continue from after its first block
+    uint64_t res[64][2 + kMaxNC];  // each one's chain through the rest of the group (St words)
+    uint64_t prim;               // which of them the primary slot's chain continues from
+    uint32_t nd;
+};
+
+// One wave: group g's table (k_sx_groups).  With more than 64 slots (a
+// block the repair pass gave exit slots), the chains of the first block's
+// slots mostly meet again where they leave it: their states after the first
+// block go to the group table, the distinct positions they continue from are
+// walked once each through the rest of the group (rounds of 64), and each
+// slot's entry is its first-block state plus its continuation's -- instead of
+// a batch of 64 chains walked through all 64 blocks per 64 slots (a group of
+// 321 slots cost ~360 us).
 template <int NC>
 __device__ void sx_group(const SxArgs& a, const uint8_t* __restrict__ w, const SxScratch& S, uint32_t pass,
-                         uint64_t g, uint8_t* stage, Chunks<NC>& mch, uint16_t* xs) {
+                         uint64_t g, uint8_t* stage, Chunks<NC>& mch, uint16_t* xs, GroupDedup<NC>& D) {
     const bool walk_prim = pass || (a.mode & 8);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t bf = g * kGroup;
@@ -2033,21 +2049,17 @@ __device__ void sx_group(const SxArgs& a, const uint8_t* __restrict__ w, const S
     const bool has3 = rl64(hv.h3, 0) != ~0ull;
     const uint32_t nx0 = nx_used(a, rl64(hv.h4, 0)), ne0 = h5_ne(rl64(hv.h5, 0));
     const uint32_t total = ns0 + (has3 ? 1 : 0) + nx0 + ne0;
+    constexpr uint32_t E = ew<NC>();
     bool miss = false, off = false;
-    uint64_t* q = S.gp + g * (kHdr + ew<NC>());
-    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
-        // lane -> slot index: window slots, the extra slot, the landing slots, the exit slots
-        const uint32_t k = k0 + lane;
-        const bool act = k < total;
-        uint32_t idx = k;
-        if (k >= ns0) {
-            const uint32_t r = k - ns0 - (has3 ? 1 : 0);  // (for k past the extra slot)
-            idx = has3 && k == ns0 ? kWin : r < nx0 ? kWin + 1 + r : kWin + 1 + kX + (r - nx0);
-        }
-        St<NC> s{};
-        s.stop = 1;  // lanes past the slots stay put
-        if (act) s = st_load<NC>(S.ent + (bf * kEnt + idx) * ew<NC>());
-        const bool primary = act && idx == prim0;
+    uint64_t* q = S.gp + g * (kHdr + E);
+    // lane -> slot index: window slots, the extra slot, the landing slots, the exit slots
+    auto slot_idx = [&](uint32_t k) -> uint32_t {
+        if (k < ns0) return k;
+        const uint32_t r = k - ns0 - (has3 ? 1 : 0);  // (for k past the extra slot)
+        return has3 && k == ns0 ? kWin : r < nx0 ? kWin + 1 + r : kWin + 1 + kX + (r - nx0);
+    };
+    // the chain state s through blocks 1 .. nbk - 1 of the group (per lane)
+    auto through_rest = [&](St<NC>& s, bool act, bool may) {
         for (uint32_t j = 1; j < nbk; ++j) {
             // chains entering block j at its primary cross its whole run at once
             const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
@@ -2055,11 +2067,98 @@ __device__ void sx_group(const SxArgs& a, const uint8_t* __restrict__ w, const S
             const uint64_t b1 = min<uint64_t>((bf + j + 1) * kSB, a.W);
             if (!__ballot(act && !st_done(s, a.W) && s.x < b1)) continue;  // every chain is past block j
             St<NC> t = s;
-            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mch, xs, primary && walk_prim);
+            through_block<NC>(a, w, S, hv, j, bf + j, t, &miss, &off, stage, &mch, xs, may);
             if (act) s = t;
         }
-        if (act) st_store<NC>(S.gent + (g * kEnt + idx) * ew<NC>(), s);
+    };
+    if (total <= 64) {
+        const uint32_t k = lane;
+        const bool act = k < total;
+        const uint32_t idx = slot_idx(k);
+        St<NC> s{};
+        s.stop = 1;  // lanes past the slots stay put
+        if (act) s = st_load<NC>(S.ent + (bf * kEnt + idx) * E);
+        const bool primary = act && idx == prim0;
+        through_rest(s, act, primary && walk_prim);
+        if (act) st_store<NC>(S.gent + (g * kEnt + idx) * E, s);
         if (primary) st_store<NC>(q + kHdr, s);  // what the in-order pass reads first
+    } else {
+        const uint64_t gend = min<uint64_t>((bf + nbk) * kSB, a.W);
+        auto pending = [&](const St<NC>& s) { return !st_done(s, a.W) && s.x < gend; };
+        // every slot's state after the first block
+        for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            if (k >= total) continue;
+            const uint32_t idx = slot_idx(k);
+            const St<NC> s = st_load<NC>(S.ent + (bf * kEnt + idx) * E);
+            st_store<NC>(S.gent + (g * kEnt + idx) * E, s);
+            if (idx == prim0 && !pending(s)) st_store<NC>(q + kHdr, s);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (;;) {
+            // up to 64 distinct continuation positions of the slots still pending
+            if (lane == 0) {
+                D.nd = 0;
+                D.prim = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            bool any = false;
+            for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                const uint32_t idx = slot_idx(k);
+                St<NC> s{};
+                bool pend = false;
+                if (k < total) {
+                    s = st_load<NC>(S.gent + (g * kEnt + idx) * E);
+                    pend = pending(s);
+                }
+                any = any || __ballot(pend);
+                uint64_t left = __ballot(pend);
+                while (left) {
+                    const uint64_t lx = rl64(s.x, __builtin_ctzll(left));
+                    const uint64_t same = __ballot(pend && s.x == lx);
+                    const uint32_t nd = D.nd;
+                    uint32_t d = nd;
+                    for (uint32_t i = 0; i < nd; ++i)
+                        if (D.ux[i] == lx) d = i;
+                    if (d == nd && nd < 64 && lane == 0) {
+                        D.ux[nd] = lx;
+                        D.nd = nd + 1;
+                    }
+                    if (d < 64 && __ballot(pend && s.x == lx && idx == prim0) && lane == 0) D.prim |= 1ull << d;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    left &= ~same;
+                }
+            }
+            if (!any) break;
+            // each distinct position's chain through the rest of the group
+            const uint32_t nd = D.nd;
+            {
+                const bool act = lane < nd;
+                St<NC> r{};
+                r.x = act ? D.ux[lane] : 0;
+                r.stop = act ? 0u : 1u;
+                through_rest(r, act, act && ((D.prim >> lane) & 1) && walk_prim);
+                if (act) st_store<NC>(D.res[lane], r);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            // every pending slot that continues from one of them: its state plus that chain
+            for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                if (k >= total) continue;
+                const uint32_t idx = slot_idx(k);
+                St<NC> s = st_load<NC>(S.gent + (g * kEnt + idx) * E);
+                if (!pending(s)) continue;
+                uint32_t d = nd;
+                for (uint32_t i = 0; i < nd; ++i)
+                    if (D.ux[i] == s.x) d = i;
+                if (d == nd) continue;  // (a later round)
+                st_add<NC>(s, st_load<NC>(D.res[d]));
+                st_store<NC>(S.gent + (g * kEnt + idx) * E, s);
+                if (idx == prim0) st_store<NC>(q + kHdr, s);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
     }
     // the first block's header words, with the primary chain above: one record
     if (lane < 6) {
@@ -2271,10 +2370,11 @@ __global__ __launch_bounds__(kBlock) void k_sx_groups(SxArgs a, const uint8_t* _
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     __shared__ uint16_t xss[kBlock / 64][kXS];
     __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
+    __shared__ GroupDedup<NC> dds[kBlock / 64];
     __shared__ uint32_t s_last;
     const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
     if (g < a.ng) sx_group<NC>(a, w, S, pass, g, stages[threadIdx.x >> 6], mchs[threadIdx.x >> 6],
-                               xss[threadIdx.x >> 6]);
+                               xss[threadIdx.x >> 6], dds[threadIdx.x >> 6]);
     // the last workgroup to finish runs the in-order scan (no waiting: the
     // others have ended; their tables are published by the fences)
     __threadfence();
