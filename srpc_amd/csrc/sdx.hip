@@ -88,11 +88,8 @@ constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
 // Exit slots (round 6, the repair pass): the live exits of every chain from
 // every position of the block before (and from longer records of blocks
 // further back), so the cursor's entry into a block is always a slot -- see
-// k_sx_fan / k_sx_exits.
+// k_sx_repair.
 constexpr uint32_t kE = 128;                     // exit slots per block
-constexpr uint32_t kNear = 256;                  // a block's live exits into the next block, at most
-constexpr uint32_t kFarIn = 64;                  // exits of longer records a block receives, at most
-constexpr uint32_t kFarSet = 256;                // k_sx_fan's set of a block's far exits (LDS hash)
 constexpr uint32_t kXS = kX + kE;                // a wave's LDS copy of a block's landing + exit slots
 constexpr uint32_t kEnt = kWin + 1 + kX + kE;    // table entries per block: the window's, the extra slot,
                                                  // the landing slots, then the exit slots
@@ -204,10 +201,6 @@ struct SxScratch {
     uint16_t* rl;    // per block, kMaxRec slots: its chunks' record starts in order (offsets from the block)
     uint16_t* xp;    // per block, kX slots: its landing slots' positions (offsets from the block, ascending)
     uint16_t* ep;    // per block, kE slots: its exit slots' positions (offsets from the block, ascending)
-    uint16_t* xnear; // per block, kNear: live exits of its chains into the next block (offsets there)
-    uint32_t* xnearc;  // per block: their count | overflow << 16
-    uint16_t* xin;   // per block, kFarIn: live exits into it of records from two or more blocks back
-    uint32_t* xinc;  // per block: their count (atomic; past kFarIn: overflow)
 };
 
 // A chain's result / the cursor's state: position (exit, or the next record
@@ -1314,10 +1307,7 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
     const uint64_t b0 = b * kSB, b1 = min<uint64_t>(b0 + kSB, W);
     SXP_BEGIN
     if (b == 0 && tid < kCtlWords) S.ctl[tid] = 0;  // this call's counters (read by the later launches)
-    if (tid == 0) {
-        L.s_nx = 0;
-        S.xinc[b] = 0;  // (the repair pass's inbox of this block, if it runs)
-    }
+    if (tid == 0) L.s_nx = 0;
     const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1, kPre);
     const StageOnlyRd so{rd};
     SXP(0);
@@ -1638,35 +1628,39 @@ __global__ __launch_bounds__(kBlock) SX_SPEC_ATTR void k_sx_spec(SxArgs a, const
 // Run only after the first scan met a position no table holds (ctl
 // kCtlRepair; otherwise every workgroup reads one word and ends).  The
 // reference's cursor enters block c at the end of the record that straddles
-// c's start: a record that starts at a position of block c - 1 (or further
-// back) the cursor reaches.  k_sx_fan takes EVERY position p of a block b:
-// the record at p, parsed in full (where one parses), links p to the next
-// record start; pointer jumping over those links in LDS (in place, at most
-// log2 of the records a block holds + 1 rounds) gives every p its exit from
-// the block -- the first record start past the block's end -- or a stop.  The
-// distinct exits at which a record parses ("live": a cursor entering anywhere
-// else stops right there, one parse) are then EVERY position the cursor can
-// enter block b + 1 at (or a later block, for a record longer than a block),
-// whatever the speculation made of block b's bytes.  k_sx_exits makes them
-// the target block's exit slots: each one's chain through the block, like the
-// table's other slots.  The second scan then meets a position no table holds
-// only where a block's exits overflowed (kNear, kFarIn, kE) or the wire is 4
-// GiB or longer: it walks those, as every miss was walked before round 6.
-// Cost: one parse per position (most stop at the first length) and the
-// jumping, for every block, in parallel -- O(bytes), no serial chain of
-// blocks.  Both kernels take blocks grid-stride from a bounded grid, so on
-// the (usual) calls that need no repair they cost two short launches.
+// c's start: a record that starts at a position of block c - 1 the cursor
+// reaches.  k_sx_repair's workgroup for block c takes EVERY position p of
+// block c - 1: the record at p, parsed in full (where one parses), links p to
+// the next record start; pointer jumping over those links in LDS (in place,
+// at most log2 of the records a block holds + 1 rounds) gives every p its
+// exit from block c - 1 -- the first record start past its end -- or a stop.
+// The distinct exits inside block c at which a record parses ("live": a
+// cursor entering anywhere else stops right there, one parse) are every
+// position the cursor can enter block c at from block c - 1, whatever the
+// speculation made of either block's bytes.  Those block c's table does not
+// already hold become its exit slots (at most kE, ascending): each one's
+// chain through block c, like the table's other chains.  The second scan
+// then meets a position no table holds only where block c had more possible
+// entries than kE, where the record that enters c started two or more blocks
+// back (longer than a block), or on a wire of 4 GiB or more (32-bit offsets):
+// those are walked, as every miss was before round 6.  Cost: one parse per
+// position (most stop at the first length) and the jumping, every block in
+// parallel -- O(bytes), no serial chain of blocks.
 constexpr uint32_t kJStop = 0xFFFFFFFFu;
-static_assert(kFarSet == 256 && kSB / 32 == kBlock, "one bitmap word / one hash slot per thread");
+static_assert(kSB / 32 == kBlock, "one bitmap word per thread");
 
-struct FanLds {
+template <int NC>
+struct RepairLds {
     alignas(16) uint8_t st[kStage + 16];
     alignas(16) uint8_t pre[kMaxPrefix + 16];
-    uint32_t J[kSB];           // per position: the next record start (< kSB: in the block), its exit, or kJStop
-    uint32_t nearm[kSB / 32];  // exits into the next block (a bit per position)
-    uint32_t far[kFarSet];     // exits past the next block, offsets from this block (0 = empty slot)
+    union {
+        uint32_t J[kSB];  // block c - 1, per position: the next record start (< kSB: in the block), its exit, kJStop
+        Chunks<NC> c;     // block c's chunks
+    } u;
+    uint32_t cand[kSB / 32];  // block c's positions: live exits of block c - 1, then those its table lacks
+    uint16_t xs[kXS];         // block c's landing slots, then (kX on) its exit slots
     uint64_t ws[kBlock / 64];
-    uint32_t far_over;
+    uint64_t zm[kZW];
 };
 
 // A record parses at x (read through the stage where it holds x).
@@ -1680,136 +1674,80 @@ __device__ __forceinline__ bool live_at(const SxArgs& a, const Rd& rd, uint64_t 
 }
 
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_fan(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+__global__ __launch_bounds__(kBlock) void k_sx_repair(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
     if (!S.ctl[kCtlRepair]) return;
-    __shared__ FanLds L;
-    const uint32_t tid = threadIdx.x;
-    for (uint64_t b = blockIdx.x; b + 1 < a.nb; b += gridDim.x) {
-        const uint64_t b0 = b * kSB, b1 = b0 + kSB;  // (never the last block: a whole one)
-        if (a.W >= kJStop) {  // offsets in 32 bits: beyond, the second scan walks
-            if (tid == 0) S.xnearc[b] = 0;
-            continue;
-        }
-        L.nearm[tid] = 0;
-        L.far[tid] = 0;
-        if (tid == 0) L.far_over = 0;
-        const StagedRd rd = stage_block(a, w, L.st, L.pre, b0, b1);  // (ends in a barrier)
-        // the record at every position: its end, relative to b0
-        for (uint32_t i = tid; i < kSB; i += kBlock) {
-            const uint64_t p = b0 + i;
-            uint32_t v = kJStop;
-            if (filter(a, rd, p)) {
-                uint32_t err;
-                uint64_t t[kMaxNC + 1];
-                const uint64_t q = parse_rd<0>(a, rd, p, &err, t);
-                if (!err) v = static_cast<uint32_t>(q - b0);
-            }
-            L.J[i] = v;
-        }
-        __syncthreads();
-        // pointer jumping: a link inside the block is replaced by its target's
-        // (a concurrent reader sees either, both on the same chain)
-        for (uint32_t r = 0; r < 32; ++r) {
-            bool more = false;
-            for (uint32_t i = tid; i < kSB; i += kBlock) {
-                uint32_t v = L.J[i];
-                if (v < kSB) {
-                    v = L.J[v];
-                    L.J[i] = v;
-                    more |= v < kSB;
-                }
-            }
-            if (!__syncthreads_or(more)) break;
-        }
-        // the distinct exits: the next block's in a bitmap, later ones in a set.
-        // Most positions share a few exits (chains converge): the lanes of a
-        // wave holding one value elect one of them, and a bit already set is
-        // not set again -- an atomic per position on the same LDS word
-        // serialised the whole block (~1 ms a block on zero-heavy bytes).
-        for (uint32_t i = tid; i < kSB; i += kBlock) {
-            const uint32_t v0 = L.J[i];
-            uint32_t v = v0 == kJStop || v0 < kSB || b0 + v0 >= a.W ? 0u : v0;  // 0: no exit to record
-            for (uint64_t act = __ballot(v != 0); act; act = __ballot(v != 0)) {
-                const uint32_t lv = __builtin_amdgcn_readlane(v, __builtin_ctzll(act));  // the lowest such lane's
-                const uint64_t mine = __ballot(v == lv);
-                if (v == lv && (threadIdx.x & 63) == static_cast<uint32_t>(__builtin_ctzll(mine))) {
-                    const uint64_t x = b0 + lv;
-                    if (x < b1 + kSB) {
-                        const uint32_t wi = static_cast<uint32_t>((x - b1) >> 5), bit = 1u << ((x - b1) & 31);
-                        if (!(L.nearm[wi] & bit)) atomicOr(&L.nearm[wi], bit);
-                    } else {
-                        uint32_t h = (lv * 2654435761u) >> 24, k = 0;
-                        for (; k < kFarSet; ++k) {
-                            const uint32_t old = atomicCAS(&L.far[h], 0u, lv);
-                            if (old == 0u || old == lv) break;
-                            h = (h + 1) & (kFarSet - 1);
-                        }
-                        if (k == kFarSet) L.far_over = 1;
-                    }
-                }
-                if (v == lv) v = 0;
-            }
-        }
-        __syncthreads();
-        // the next block's live exits, in order (a bitmap word per thread)
-        uint32_t m = L.nearm[tid], live = 0;
-        while (m) {
-            const uint32_t bit = __builtin_ctz(m);
-            m &= m - 1;
-            if (live_at(a, rd, b1 + 32 * tid + bit)) live |= 1u << bit;
-        }
-        uint64_t tot;
-        uint64_t k = block_xscan(__builtin_popcount(live), &tot, L.ws);
-        while (live) {
-            const uint32_t bit = __builtin_ctz(live);
-            live &= live - 1;
-            if (k < kNear) S.xnear[b * kNear + k] = static_cast<uint16_t>(32 * tid + bit);
-            ++k;
-        }
-        // the later blocks' live exits, into their inboxes (a set slot per thread)
-        const uint32_t v = L.far[tid];
-        if (v) {
-            const uint64_t x = b0 + v;
-            if (live_at(a, rd, x)) {
-                const uint64_t t = x / kSB;
-                const uint32_t j = atomicAdd(&S.xinc[t], 1u);
-                if (j < kFarIn) S.xin[t * kFarIn + j] = static_cast<uint16_t>(x - t * kSB);
-            }
-        }
-        if (tid == 0) {
-            S.xnearc[b] = static_cast<uint32_t>(min<uint64_t>(tot, kNear)) | (tot > kNear ? 1u << 16 : 0u);
-            if (L.far_over) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOver]), 1ull);
-        }
-        __syncthreads();  // (the next block's stage overwrites this one's LDS)
-    }
-}
-
-template <int NC>
-struct ExitLds {
-    alignas(16) uint8_t st[kStage + 16];
-    alignas(16) uint8_t pre[kMaxPrefix + 16];
-    Chunks<NC> c;
-    uint16_t xs[kXS];                 // the block's landing slots, then (kX on) its exit slots
-    uint32_t keep[kSB / 32];          // the candidates its table does not hold (a bit per position)
-    uint64_t ws[kBlock / 64];
-    uint64_t zm[kZW];
-};
-
-// Block c's exit slots: the live exits of block c - 1's chains into it and of
-// longer records' into it (k_sx_fan), minus the positions its table already
-// holds, sorted, at most kE; each one's chain through the block, as the
-// table's other chains (the chunks walked again from phase 1's starts).
-template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
-    if (!S.ctl[kCtlRepair]) return;
-    __shared__ ExitLds<NC> L;
+    __shared__ RepairLds<NC> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     for (uint64_t c = 1 + blockIdx.x; c < a.nb; c += gridDim.x) {
-        const uint32_t xn = S.xnearc[c - 1], fin = S.xinc[c];
-        const uint32_t nn = min<uint32_t>(xn & 0xffff, kNear), nf = min<uint32_t>(fin, kFarIn), nc = nn + nf;
-        if (nc == 0) continue;  // (uniform: every thread read the same words)
+        if (a.W >= kJStop) break;  // offsets in 32 bits: beyond, the second scan walks
+        // ---- block c - 1: every position's exit
+        const uint64_t p0 = (c - 1) * kSB, p1 = p0 + kSB;  // (a whole block: not the last)
+        L.cand[tid] = 0;
+        {
+            const StagedRd rd = stage_block(a, w, L.st, L.pre, p0, p1);  // (ends in a barrier)
+            for (uint32_t i = tid; i < kSB; i += kBlock) {
+                const uint64_t p = p0 + i;
+                uint32_t v = kJStop;
+                if (filter(a, rd, p)) {
+                    uint32_t err;
+                    uint64_t t[kMaxNC + 1];
+                    const uint64_t q = parse_rd<0>(a, rd, p, &err, t);
+                    if (!err) v = static_cast<uint32_t>(q - p0);
+                }
+                L.u.J[i] = v;
+            }
+            __syncthreads();
+            // pointer jumping: a link inside the block is replaced by its
+            // target's (a concurrent reader sees either, both on one chain)
+            for (uint32_t r = 0; r < 32; ++r) {
+                bool more = false;
+                for (uint32_t i = tid; i < kSB; i += kBlock) {
+                    uint32_t v = L.u.J[i];
+                    if (v < kSB) {
+                        v = L.u.J[v];
+                        L.u.J[i] = v;
+                        more |= v < kSB;
+                    }
+                }
+                if (!__syncthreads_or(more)) break;
+            }
+            // the distinct exits into block c, a bit per position.  Most
+            // positions share a few exits (chains converge): the lanes of a
+            // wave holding one value elect one of them, and a bit already set
+            // is not set again (an atomic per position on one LDS word
+            // serialised the whole block: ~1 ms a block on zero-heavy bytes)
+            for (uint32_t i = tid; i < kSB; i += kBlock) {
+                const uint32_t v0 = L.u.J[i];
+                // an exit into block c, as its offset there + 1 (0: none)
+                uint32_t v = v0 == kJStop || v0 < kSB || v0 >= 2 * kSB || p0 + v0 >= a.W ? 0u : v0 - kSB + 1;
+                for (uint64_t act = __ballot(v != 0); act; act = __ballot(v != 0)) {
+                    const uint32_t lv = __builtin_amdgcn_readlane(v, __builtin_ctzll(act));
+                    const uint64_t mine = __ballot(v == lv);
+                    if (v == lv && lane == static_cast<uint32_t>(__builtin_ctzll(mine))) {
+                        const uint32_t o = lv - 1, wi = o >> 5, bit = 1u << (o & 31);
+                        if (!(L.cand[wi] & bit)) atomicOr(&L.cand[wi], bit);
+                    }
+                    if (v == lv) v = 0;
+                }
+            }
+            __syncthreads();
+            // live ones only (a bitmap word per thread)
+            uint32_t m = L.cand[tid], live = 0;
+            while (m) {
+                const uint32_t bit = __builtin_ctz(m);
+                m &= m - 1;
+                if (live_at(a, rd, p1 + 32 * tid + bit)) live |= 1u << bit;
+            }
+            L.cand[tid] = live;
+        }
+        const uint32_t any = __syncthreads_or(L.cand[tid] != 0);  // (also: the stage is free)
+        if (!any) {
+            if (tid == 0) S.hdr[kHdr * c + 5] = 0;
+            __syncthreads();
+            continue;
+        }
+        // ---- block c: the candidates its table does not hold, their chains
         const uint64_t b0 = c * kSB, b1 = min<uint64_t>(b0 + kSB, a.W);
-        L.keep[tid] = 0;
         const uint64_t* h = S.hdr + kHdr * c;
         const uint64_t h0 = h[0], h1 = h[1], h3 = h[3], h4 = h[4];
         const uint32_t meta = static_cast<uint32_t>(h[2]), nx = nx_used(a, h4);
@@ -1823,7 +1761,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __
         uint32_t ccnt, cstop;
         uint64_t cexit;
         walk_chunk<NC>(a, rd, sp, chi, &ccnt, &cexit, cch, &cstop, nullptr);
-        Chunks<NC>& C = L.c;
+        Chunks<NC>& C = L.u.c;
         C.start[tid] = sp == ~0ull ? kNoStart : static_cast<uint16_t>(sp - b0);
         C.exit[tid] = cexit;
         C.stop[tid] = static_cast<uint8_t>(cstop);
@@ -1831,27 +1769,24 @@ __global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __
         if (lane == 0) C.has[tid >> 6] = hm;
         __syncthreads();
         link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);  // (ends in a barrier)
-        // the candidates the table does not hold yet, deduplicated (a near exit
-        // can also arrive as a far one) and sorted by a bitmap
-        for (uint32_t i = tid; i < nc; i += kBlock) {
-            const uint32_t o = i < nn ? S.xnear[(c - 1) * kNear + i] : S.xin[c * kFarIn + (i - nn)];
-            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0)
-                atomicOr(&L.keep[o >> 5], 1u << (o & 31));
-        }
-        __syncthreads();
-        uint32_t m = L.keep[tid];
-        uint64_t tot;
-        uint64_t k = block_xscan(__builtin_popcount(m), &tot, L.ws);
+        uint32_t m = L.cand[tid], keep = 0;
         while (m) {
             const uint32_t bit = __builtin_ctz(m);
             m &= m - 1;
+            const uint32_t o = 32 * tid + bit;
+            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0) keep |= 1u << bit;
+        }
+        uint64_t tot;
+        uint64_t k = block_xscan(__builtin_popcount(keep), &tot, L.ws);
+        while (keep) {
+            const uint32_t bit = __builtin_ctz(keep);
+            keep &= keep - 1;
             if (k < kE) L.xs[kX + k] = static_cast<uint16_t>(32 * tid + bit);
             ++k;
         }
-        const uint32_t ne = static_cast<uint32_t>(min<uint64_t>(tot, 0xffff));
         __syncthreads();
-        const uint32_t nu = min(ne, kE);
-        const bool zf = ((meta >> 17) & 1) && NC < 3;  // a zero-heavy block: chains cross zero runs by its zero map
+        const uint32_t nu = static_cast<uint32_t>(min<uint64_t>(tot, kE));
+        const bool zf = ((meta >> 17) & 1) && NC < 3;  // a mostly-zero block: chains cross zero runs by its map
         if (zf) build_zmap(rd, b0, L.zm);
         for (uint32_t j = tid; j < nu; j += kBlock) {
             const uint32_t o = L.xs[kX + j];
@@ -1861,7 +1796,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_exits(SxArgs a, const uint8_t* __
             S.ep[c * kE + j] = static_cast<uint16_t>(o);
         }
         if (tid == 0) {
-            const bool over = ne > kE || (xn >> 16) || fin > kFarIn;
+            const bool over = tot > kE;
             S.hdr[kHdr * c + 5] = nu | (over ? 1u << 8 : 0u);
             if (over) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOver]), 1ull);
         }
@@ -2397,24 +2332,18 @@ __global__ __launch_bounds__(64) void k_sx_top(SxArgs a, const uint8_t* __restri
     sx_top<NC, kDecode>(a, w, S, st, pass, stage, mch, xs);
 }
 
-// A wave per group: every block's entry state, from the group's.
+// One wave: every block's entry state of group g, from the group's.
 template <int NC>
-__global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
+__device__ void sx_blocks_group(const SxArgs& a, const uint8_t* __restrict__ w, const SxScratch& S, uint64_t g,
+                                uint8_t* stage, Chunks<NC>& mch, uint16_t* xs) {
     constexpr uint32_t E = ew<NC>();
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-    if (g >= a.ng) return;
     const uint64_t bf = g * kGroup;
     const uint32_t nbk = static_cast<uint32_t>(min<uint64_t>(kGroup, a.nb - bf));
     Held<NC> hv;
     hv.load(S, bf + lane, lane < nbk, nbk);
     St<NC> s = st_load<NC>(S.gin + g * E);
     uint64_t out[E];
-    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
-    __shared__ uint16_t xss[kBlock / 64][kXS];
-    uint8_t* stage = stages[threadIdx.x >> 6];
-    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
-    uint16_t* xs = xss[threadIdx.x >> 6];
     bool miss = false, off = false;
     for (uint32_t j = 0; j < nbk;) {
         const bool hp = __builtin_amdgcn_readlane(static_cast<uint32_t>(hv.has_prim), j);
@@ -2444,7 +2373,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
         st_store<NC>(v, s);
 #pragma unroll
         for (uint32_t k = 0; k < E; ++k) out[k] = lane == j ? v[k] : out[k];
-        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage, &mchs[threadIdx.x >> 6], xs);
+        through_block<NC>(a, w, S, hv, j, bf + j, s, &miss, &off, stage, &mch, xs);
         ++j;
     }
     if (lane < nbk)
@@ -2452,6 +2381,41 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
         for (uint32_t k = 0; k < E; ++k) S.bst[(bf + lane) * E + k] = out[k];
     if (lane == 0 && miss) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlMiss]), 1ull);
     if (lane == 0 && off) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOff]), 1ull);
+}
+
+// A wave per group: every block's entry state (sx_blocks_group).  After a
+// repair (ctl kCtlRepair) the same launch is the second scan first: every
+// group's table again (sx_group, pass 1), then in the last workgroup to finish
+// the in-order scan and every group's block states, its four waves taking the
+// groups in turn -- so a call that needs no repair pays for no extra launch
+// of the second scan.
+template <int NC, bool kDecode>
+__global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
+                                                      srpc_unpack_status* st) {
+    __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
+    __shared__ uint16_t xss[kBlock / 64][kXS];
+    __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
+    __shared__ GroupDedup<NC> dds[kBlock / 64];
+    __shared__ uint32_t s_last;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv;
+    if (!S.ctl[kCtlRepair]) {
+        if (g < a.ng) sx_blocks_group<NC>(a, w, S, g, stages[wv], mchs[wv], xss[wv]);
+        return;
+    }
+    if (g < a.ng) sx_group<NC>(a, w, S, 1, g, stages[wv], mchs[wv], xss[wv], dds[wv]);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlDone + 1]), 1ull) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (wv == 0) sx_top<NC, kDecode>(a, w, S, st, 1, stages[0], mchs[0], xss[0]);
+    __threadfence();
+    __syncthreads();
+    __threadfence();
+    for (uint64_t gg = wv; gg < a.ng; gg += kBlock / 64) sx_blocks_group<NC>(a, w, S, gg, stages[wv], mchs[wv], xss[wv]);
 }
 
 // ---- phase 3: the records of every block ----------------------------------------
@@ -2812,7 +2776,7 @@ __global__ void k_zero_ctl(uint64_t* ctl) {
 uint64_t r256(uint64_t b) { return (b + 255) & ~255ull; }
 
 struct SxLayout {
-    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, xp, ep, xnear, xnearc, xin, xinc, total;
+    uint64_t nb, ng, spec, hdr, ent, gent, gp, gin, bst, ctl, rl, xp, ep, total;
 };
 
 SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
@@ -2843,14 +2807,6 @@ SxLayout sx_layout(uint64_t wire_len, uint32_t nc) {
     o += r256(2 * kX * L.nb);
     L.ep = o;
     o += r256(2 * kE * L.nb);
-    L.xnear = o;
-    o += r256(2 * kNear * L.nb);
-    L.xnearc = o;
-    o += r256(4 * L.nb);
-    L.xin = o;
-    o += r256(2 * kFarIn * L.nb);
-    L.xinc = o;
-    o += r256(4 * L.nb);
     L.total = o;
     return L;
 }
@@ -2867,16 +2823,13 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
     // the groups' tables, then (their last workgroup) the in-order scan
     if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 0u);
     else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
-    // the repair pass and the second scan: each workgroup reads one control
-    // word and ends unless the first scan asked for them (a bounded grid)
-    if (a.nb > 1) {
-        const uint32_t rg = static_cast<uint32_t>(std::min<uint64_t>(a.nb, 1024));
-        launch(k_sx_fan<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
-        launch(k_sx_exits<NC>, dim3(rg), dim3(kBlock), 0, s, a, wire, S);
-    }
-    if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 1u);
-    else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 1u);
-    if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
+    // the repair pass: each workgroup reads one control word and ends unless
+    // the first scan asked for it (a bounded grid); then the blocks' states,
+    // which after a repair are the second scan first (k_sx_blocks)
+    if (a.nb > 1)
+        launch(k_sx_repair<NC>, dim3(static_cast<uint32_t>(std::min<uint64_t>(a.nb - 1, 1024))), dim3(kBlock), 0, s, a,
+               wire, S);
+    if (a.ng) launch(k_sx_blocks<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st);
     const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
     launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
 }
@@ -2929,11 +2882,7 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
                 reinterpret_cast<uint64_t*>(base + SL.ctl),
                 reinterpret_cast<uint16_t*>(base + SL.rl),
                 reinterpret_cast<uint16_t*>(base + SL.xp),
-                reinterpret_cast<uint16_t*>(base + SL.ep),
-                reinterpret_cast<uint16_t*>(base + SL.xnear),
-                reinterpret_cast<uint32_t*>(base + SL.xnearc),
-                reinterpret_cast<uint16_t*>(base + SL.xin),
-                reinterpret_cast<uint32_t*>(base + SL.xinc)};
+                reinterpret_cast<uint16_t*>(base + SL.ep)};
     SxArgs a{};
     uint32_t si = 0;
     for (uint32_t f = 0; f < p->nfields; ++f) {
