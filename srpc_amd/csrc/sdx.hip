@@ -2383,39 +2383,15 @@ __device__ void sx_blocks_group(const SxArgs& a, const uint8_t* __restrict__ w, 
     if (lane == 0 && off) atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlOff]), 1ull);
 }
 
-// A wave per group: every block's entry state (sx_blocks_group).  After a
-// repair (ctl kCtlRepair) the same launch is the second scan first: every
-// group's table again (sx_group, pass 1), then in the last workgroup to finish
-// the in-order scan and every group's block states, its four waves taking the
-// groups in turn -- so a call that needs no repair pays for no extra launch
-// of the second scan.
-template <int NC, bool kDecode>
-__global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* __restrict__ w, SxScratch S,
-                                                      srpc_unpack_status* st) {
+// A wave per group: every block's entry state (sx_blocks_group).
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* __restrict__ w, SxScratch S) {
     __shared__ __attribute__((aligned(16))) uint8_t stages[kBlock / 64][kWaveStage + 16];
     __shared__ uint16_t xss[kBlock / 64][kXS];
     __shared__ Chunks<NC> mchs[kBlock / 64];  // walk_miss's chunks, one set per wave
-    __shared__ GroupDedup<NC> dds[kBlock / 64];
-    __shared__ uint32_t s_last;
     const uint32_t wv = threadIdx.x >> 6;
     const uint64_t g = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv;
-    if (!S.ctl[kCtlRepair]) {
-        if (g < a.ng) sx_blocks_group<NC>(a, w, S, g, stages[wv], mchs[wv], xss[wv]);
-        return;
-    }
-    if (g < a.ng) sx_group<NC>(a, w, S, 1, g, stages[wv], mchs[wv], xss[wv], dds[wv]);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_last = atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[kCtlDone + 1]), 1ull) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (wv == 0) sx_top<NC, kDecode>(a, w, S, st, 1, stages[0], mchs[0], xss[0]);
-    __threadfence();
-    __syncthreads();
-    __threadfence();
-    for (uint64_t gg = wv; gg < a.ng; gg += kBlock / 64) sx_blocks_group<NC>(a, w, S, gg, stages[wv], mchs[wv], xss[wv]);
+    if (g < a.ng) sx_blocks_group<NC>(a, w, S, g, stages[wv], mchs[wv], xss[wv]);
 }
 
 // ---- phase 3: the records of every block ----------------------------------------
@@ -2823,13 +2799,14 @@ void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_un
     // the groups' tables, then (their last workgroup) the in-order scan
     if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 0u);
     else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
-    // the repair pass: each workgroup reads one control word and ends unless
-    // the first scan asked for it (a bounded grid); then the blocks' states,
-    // which after a repair are the second scan first (k_sx_blocks)
+    // the repair pass and the second scan: each workgroup reads one control
+    // word and ends unless the first scan asked for them (the repair from a
+    // bounded grid); then every block's state
     if (a.nb > 1)
         launch(k_sx_repair<NC>, dim3(static_cast<uint32_t>(std::min<uint64_t>(a.nb - 1, 1024))), dim3(kBlock), 0, s, a,
                wire, S);
-    if (a.ng) launch(k_sx_blocks<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st);
+    if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 1u);
+    if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
     const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
     launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
 }
