@@ -89,7 +89,7 @@ constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
 // every position of the block before (and from longer records of blocks
 // further back), so the cursor's entry into a block is always a slot -- see
 // k_sx_repair.
-constexpr uint32_t kE = 128;                     // exit slots per block
+constexpr uint32_t kE = 255;                     // exit slots per block (header word 5 counts them in 8 bits)
 constexpr uint32_t kXS = kX + kE;                // a wave's LDS copy of a block's landing + exit slots
 constexpr uint32_t kEnt = kWin + 1 + kX + kE;    // table entries per block: the window's, the extra slot,
                                                  // the landing slots, then the exit slots
