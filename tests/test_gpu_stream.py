@@ -374,8 +374,13 @@ def test_straddling_records_at_every_block(n, lead, over, fill, path):
         assert r >> 8 == 0 and not r & RES_REPAIR, (r >> 8, len(wire) // 8192)
     elif path == "walk_norepair" and len(wire) > 64 * 8192:
         assert r & RES_MISS, r
-    elif path != "walk_norepair":  # the repair pass ran where it had to, and nothing was walked
-        assert r >> 8 == 0, (r, len(wire) // 8192)
+    elif path != "walk_norepair":
+        # the repair pass ran where it had to, and nothing was walked unless a
+        # block had more possible entries than its exit slots hold (reserved
+        # bit 3: a few blocks of zero-filled straddlers in the test-hook modes,
+        # where the zero-run rule is off)
+        assert r >> 8 == 0 or r & RES_OVER, (r, len(wire) // 8192)
+        assert r >> 8 <= len(wire) // 8192 // 1000 + 1, (r, len(wire) // 8192)
 
 
 def test_records_across_block_edges_and_margin(path):
