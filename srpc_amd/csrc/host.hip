@@ -500,3 +500,11 @@ extern "C" __attribute__((visibility("default"))) void srpc_debug_host_fail_at(u
 extern "C" __attribute__((visibility("default"))) uint64_t srpc_debug_host_last_pipe(void) {
     return reinterpret_cast<uintptr_t>(t_last_pipe);
 }
+
+// Test hook: how many pipes this process has made (every device).
+extern "C" __attribute__((visibility("default"))) uint64_t srpc_debug_host_pipes_made(void) {
+    std::lock_guard<std::mutex> lk(pool().mu);
+    uint64_t n = 0;
+    for (const auto& kv : pool().made) n += kv.second;
+    return n;
+}

@@ -48,6 +48,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 
@@ -1663,6 +1664,46 @@ struct RepairLds {
     uint64_t zm[kZW];
 };
 
+// The end of the record at p when it parses and ends at most at `limit`;
+// otherwise p with *far set when it would end past `limit` (its exit cannot
+// be an entry of the next block: the repair ignores it, so a record whose
+// first string alone runs past the limit costs no read of the far bytes its
+// later fields would need) or *err set when it does not parse.
+template <class Rd>
+__device__ __forceinline__ uint64_t parse_near(const SxArgs& a, const Rd& r, uint64_t p, uint64_t limit, bool* bad) {
+    const uint64_t W = a.W;
+    bool e = false;
+    if (a.prefix_len) {
+        if (a.prefix_len > W - p) {
+            e = true;
+        } else {
+            uint64_t diff = 0;
+            uint32_t i = 0;
+            for (; i + 8 <= a.prefix_len; i += 8) diff |= r.u64(p + i) ^ r.pre64(i);
+            for (; i < a.prefix_len; ++i) diff |= r.u8(p + i) ^ r.pre8(i);
+            e = diff != 0;
+        }
+    }
+    uint64_t q = p;
+    for (uint32_t k = 0; k < a.nstrings; ++k) {
+        const uint32_t g = a.gap[k] + 8;
+        if (!e) {
+            if (g > W - q || q + g > limit) {
+                e = true;
+            } else {
+                q += g;
+                const uint64_t len = r.u64(q - 8);
+                if (len > W - q || len > limit - q) e = true;
+                else q += len;
+            }
+        }
+    }
+    const uint32_t gl = a.gap[a.nstrings];
+    if (!e && (gl > W - q || q + gl > limit)) e = true;
+    *bad = e;
+    return e ? p : q + gl;
+}
+
 // A record parses at x (read through the stage where it holds x).
 template <class Rd>
 __device__ __forceinline__ bool live_at(const SxArgs& a, const Rd& rd, uint64_t x) {
@@ -1685,14 +1726,16 @@ __global__ __launch_bounds__(kBlock) void k_sx_repair(SxArgs a, const uint8_t* _
         L.cand[tid] = 0;
         {
             const StagedRd rd = stage_block(a, w, L.st, L.pre, p0, p1);  // (ends in a barrier)
+            // (a record that would end past block c: a stop here -- its exit
+            // and those of the chains through it are not entries of block c)
+            const uint64_t lim = min<uint64_t>(p1 + kSB, a.W);
             for (uint32_t i = tid; i < kSB; i += kBlock) {
                 const uint64_t p = p0 + i;
                 uint32_t v = kJStop;
                 if (filter(a, rd, p)) {
-                    uint32_t err;
-                    uint64_t t[kMaxNC + 1];
-                    const uint64_t q = parse_rd<0>(a, rd, p, &err, t);
-                    if (!err) v = static_cast<uint32_t>(q - p0);
+                    bool bad;
+                    const uint64_t q = parse_near(a, rd, p, lim, &bad);
+                    if (!bad) v = static_cast<uint32_t>(q - p0);
                 }
                 L.u.J[i] = v;
             }
@@ -1731,14 +1774,6 @@ __global__ __launch_bounds__(kBlock) void k_sx_repair(SxArgs a, const uint8_t* _
                 }
             }
             __syncthreads();
-            // live ones only (a bitmap word per thread)
-            uint32_t m = L.cand[tid], live = 0;
-            while (m) {
-                const uint32_t bit = __builtin_ctz(m);
-                m &= m - 1;
-                if (live_at(a, rd, p1 + 32 * tid + bit)) live |= 1u << bit;
-            }
-            L.cand[tid] = live;
         }
         const uint32_t any = __syncthreads_or(L.cand[tid] != 0);  // (also: the stage is free)
         if (!any) {
@@ -1769,12 +1804,15 @@ __global__ __launch_bounds__(kBlock) void k_sx_repair(SxArgs a, const uint8_t* _
         if (lane == 0) C.has[tid >> 6] = hm;
         __syncthreads();
         link_chunks<NC>(C, b0, sp, cexit, cstop, ccnt, cch);  // (ends in a barrier)
+        // the live exits (a record parses there: read from this block's
+        // stage) its table does not hold
         uint32_t m = L.cand[tid], keep = 0;
         while (m) {
             const uint32_t bit = __builtin_ctz(m);
             m &= m - 1;
             const uint32_t o = 32 * tid + bit;
-            if (find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0) keep |= 1u << bit;
+            if (live_at(a, rd, b0 + o) && find_slot(a, h0, h1, h3, meta, h4, 0, L.xs, b0, b0 + o).idx < 0)
+                keep |= 1u << bit;
         }
         uint64_t tot;
         uint64_t k = block_xscan(__builtin_popcount(keep), &tot, L.ws);
@@ -2793,22 +2831,38 @@ bool sx_decodes(const srpc_plan* p) { return p->nstrings <= kMaxNC + 1; }
 
 template <int NC, bool kDecode>
 void launch_sx(const SxArgs& a, const uint8_t* wire, const SxScratch& S, srpc_unpack_status* st, hipStream_t s) {
+    // test hook 16: wait for each kernel and name the first that fails
+    bool ok = true;
+    auto done = [&](const char* k) {
+        if (!(a.mode & 16) || !ok) return;
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            ok = false;
+            std::fprintf(stderr, "srpc sdx: %s<%d>: %s\n", k, NC, hipGetErrorString(e));
+        }
+    };
     if (a.nb) launch(k_sx_spec<NC>, dim3(a.nb), dim3(kBlock), 0, s, a, wire, S);
     else hipLaunchKernelGGL(k_zero_ctl, dim3(1), dim3(64), 0, s, S.ctl);
+    done("spec");
     const uint32_t gw = (a.ng + kBlock / 64 - 1) / (kBlock / 64);
     // the groups' tables, then (their last workgroup) the in-order scan
     if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 0u);
     else launch(k_sx_top<NC, kDecode>, dim3(1), dim3(64), 0, s, a, wire, S, st, 0u);
+    done("groups0");
     // the repair pass and the second scan: each workgroup reads one control
     // word and ends unless the first scan asked for them (the repair from a
     // bounded grid); then every block's state
     if (a.nb > 1)
         launch(k_sx_repair<NC>, dim3(static_cast<uint32_t>(std::min<uint64_t>(a.nb - 1, 1024))), dim3(kBlock), 0, s, a,
                wire, S);
+    done("repair");
     if (a.ng) launch(k_sx_groups<NC, kDecode>, dim3(gw), dim3(kBlock), 0, s, a, wire, S, st, 1u);
+    done("groups1");
     if (a.ng) launch(k_sx_blocks<NC>, dim3(gw), dim3(kBlock), 0, s, a, wire, S);
+    done("blocks");
     const uint32_t g = static_cast<uint32_t>(std::max<uint64_t>(a.nb, 1));
     launch(k_sx_decode<NC, kDecode>, dim3(g), dim3(kBlock), 0, s, a, wire, S, st);
+    done("decode");
 }
 
 }  // namespace
@@ -2915,7 +2969,8 @@ int srpc_gpu_unpack_var_stream(const srpc_plan* p, const uint8_t* wire, uint64_t
 // exit slots, or a walk), 2 = empty tables (every block entered needs them),
 // 4 = the speculation's exact filter at every position instead of zero-byte
 // candidates, 8 = no repair pass (a position no table holds is walked, the
-// round-5 path); 0 = normal.  Returns the previous setting.
+// round-5 path), 16 = wait for each kernel and name the first that fails on
+// stderr; 0 = normal.  Returns the previous setting.
 #ifdef SRPC_SX_PHASES
 extern "C" int srpc_debug_sx_phases(void* d_buf, uint64_t nblocks) {
     unsigned long long* p = static_cast<unsigned long long*>(d_buf);
@@ -2927,5 +2982,5 @@ extern "C" int srpc_debug_sx_phases(void* d_buf, uint64_t nblocks) {
 #endif
 
 extern "C" __attribute__((visibility("default"))) int srpc_debug_stream_tables(int mode) {
-    return static_cast<int>(srpc_impl::g_sx_mode.exchange(static_cast<uint32_t>(mode < 0 ? 0 : mode > 15 ? 15 : mode)));
+    return static_cast<int>(srpc_impl::g_sx_mode.exchange(static_cast<uint32_t>(mode < 0 ? 0 : mode > 31 ? 31 : mode)));
 }

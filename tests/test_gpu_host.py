@@ -261,8 +261,9 @@ def test_host_pipes_not_shared_across_streams_while_busy():
     enqueued, long before its copies finish.  A call on ANOTHER caller stream
     must not take that busy pipe (its copies would queue behind the first
     call's on the same internal streams); a call on the SAME stream may (its
-    work is ordered behind the first call's anyway); once the first call has
-    drained, any stream may reuse it."""
+    work is ordered behind the first call's anyway); once the calls have
+    drained, a call on any stream reuses an idle pipe (one of these or an
+    earlier test's) instead of making one."""
     import ctypes
     last = _hook("srpc_debug_host_last_pipe", ctypes.c_uint64, [])
     kinds, p = plan("quad")
@@ -287,8 +288,10 @@ def test_host_pipes_not_shared_across_streams_while_busy():
     if busy:
         assert a != b, "a busy pipe was lent to a call on another stream"
     assert c == a, "a call on the same stream should reuse that stream's pipe"
+    made = _hook("srpc_debug_host_pipes_made", ctypes.c_uint64, [])
+    before = made()
     p.pack_host(h_cols, n, wires[1], chunk, keep[1][1], keep[1][2], depth=3, stream=torch.cuda.Stream())
-    assert last() in (a, b), "an idle pipe should be reused, not a new one made"
+    assert made() == before, "an idle pipe should be reused, not a new one made"
     torch.cuda.synchronize()
 
 
