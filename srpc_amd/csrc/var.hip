@@ -489,7 +489,7 @@ struct SingleFast {
     uint64_t* soff1;       // str_offs of the string field (n + 1)
     uint64_t* tiles;       // chars tiles' first records
     uint64_t max_tiles;
-    uint32_t* bad;         // [0] some record is not exact
+    uint32_t* bad;         // [0] some record is not exact, [16] some chars tile is left to the chars kernel
     uint8_t* chars;        // the string field's output chars
     uint32_t* tile_long;   // per chars tile: 1 = it holds chars the walk did not copy
     uint32_t chars_at;     // chars start this many bytes into a record
@@ -717,7 +717,8 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
         const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end && start >= first &&
                            start - first >= r * a.fixed_bytes && o <= wire_len && len <= wire_len - o;
         // a wave whose strings are all short copies them here; otherwise its
-        // strings' chars tiles are left to k_unpack_var_chars
+        // strings' chars tiles are left to k_unpack_var_chars (bad[16] says
+        // some tile is, else that launch has nothing to do)
         const bool all_short = __all(exact && len <= kShortCopy);
         if (exact) {
             for (uint64_t t = (o + kTileBytes - 1) / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
@@ -727,6 +728,7 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
             } else {
                 for (uint64_t t = o / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
                     fast.tile_long[t] = 1;
+                fast.bad[16] = 1;
             }
         } else {
             atomicOr(fast.bad, 1u);
@@ -751,6 +753,7 @@ constexpr uint64_t kWalkStageMax = 49152;
 #ifndef SRPC_RTU_OFFLOAD
 #define SRPC_RTU_OFFLOAD 1  // look-back waves' records built by the other waves (two strings 279 -> 270 us)
 #endif
+constexpr uint64_t kWalkTwoPerLane = 20;  // single-string walk: two records per lane at most this average
 #ifndef SRPC_STAGE_DEN
 #define SRPC_STAGE_DEN 16
 #endif
@@ -766,15 +769,16 @@ static_assert(SRPC_STAGE_NUM >= SRPC_STAGE_DEN, "the stage must hold at least th
 // correct either way).  5/4 rounded to 4 KiB staged 32 KiB for ~100-byte
 // records (4 workgroups per CU); 17/16 rounded to 512 B stages 27.5 KiB (5):
 // two strings + envelope unpack 380 -> 361 us (r01_var_stage_slack_ab.log).
-inline uint64_t stage_bytes_for(uint64_t avg) {
-    return (avg * kBlock * SRPC_STAGE_NUM / SRPC_STAGE_DEN + 32 + SRPC_STAGE_ROUND - 1) & ~(SRPC_STAGE_ROUND - 1ull);
+inline uint64_t stage_bytes_for(uint64_t avg, uint32_t rpl = 1) {
+    return (avg * kBlock * rpl * SRPC_STAGE_NUM / SRPC_STAGE_DEN + 32 + SRPC_STAGE_ROUND - 1) &
+           ~(SRPC_STAGE_ROUND - 1ull);
 }
 
 // STAGED (chosen by the host when 17/16 of the average span fits 48 KiB): the
 // stage is dynamic LDS of exactly stage_bytes -- a fixed 32 KiB stage cost
 // short-record schemas more in occupancy than it saved (0-16 B strings
 // 105 -> 139 us), the sized one gains 4-8 % on them.
-template <bool STAGED>
+template <bool STAGED, int RPL>
 __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uint8_t* __restrict__ wire,
                                                             uint64_t wire_len, const uint64_t* __restrict__ rec_offs,
                                                             uint64_t n, uint64_t* lens, uint64_t* spos,
@@ -783,8 +787,23 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
     __shared__ __attribute__((aligned(16))) uint8_t pre[kMaxPrefix + 16];
     extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
     for (uint32_t i = threadIdx.x; i < a.prefix_len; i += kBlock) pre[i] = a.prefix[i];
-    const uint64_t rA = static_cast<uint64_t>(blockIdx.x) * kBlock;
-    const uint64_t rB = min<uint64_t>(rA + kBlock, n);
+    constexpr uint64_t kRecs = static_cast<uint64_t>(kBlock) * RPL;
+    const uint64_t rA = static_cast<uint64_t>(blockIdx.x) * kRecs;
+    const uint64_t rB = min<uint64_t>(rA + kRecs, n);
+    // the lanes' own record bounds are loaded with the span's, before the
+    // stage's barrier (one memory round trip less per workgroup: 0-16 B
+    // strings 108.6 -> 99.2 us, profiles/r06_var_walk_ab.log)
+    uint64_t start[RPL], end[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+        const uint64_t r = rA + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+        start[j] = r < n ? rec_offs[r] : 0;
+        end[j] = r < n ? rec_offs[r + 1] : 0;
+    }
+    if (fast.soff1) {
+        fast.first = rec_offs[0];
+        fast.last = rec_offs[n];
+    }
     const uint64_t lo = rec_offs[rA], hi = min(rec_offs[rB], wire_len);
     const uint64_t base = lo & ~15ull;
     // 16 bytes past the span: a fixed field after a string may be read up to
@@ -803,21 +822,19 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_walk(VarArgs a, const uin
         }
     }
     __syncthreads();
-    const uint64_t r = rA + threadIdx.x;
-    const bool valid = r < n;
-    const uint64_t start = valid ? rec_offs[r] : 0, end = valid ? rec_offs[r + 1] : 0;
-    if (fast.soff1) {
-        fast.first = rec_offs[0];
-        fast.last = rec_offs[n];
-    }
     // (walk_record's all-short vote then runs per branch: it only chooses
     // between a lane copying its own string and flagging its chars tiles,
     // and either is correct per lane)
-    if (staged && valid && start >= lo && end <= hi && start <= end) {
-        walk_record(a, stage + (start - base), stage + (shi - base), pre, r, start, end, wire_len, n, lens, spos,
-                    st, fast);
-    } else if (valid) {
-        walk_record(a, wire + start, wire + wire_len, pre, r, start, end, wire_len, n, lens, spos, st, fast);
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+        const uint64_t r = rA + static_cast<uint64_t>(j) * kBlock + threadIdx.x;
+        if (r >= n) continue;
+        if (staged && start[j] >= lo && end[j] <= hi && start[j] <= end[j])
+            walk_record(a, stage + (start[j] - base), stage + (shi - base), pre, r, start[j], end[j], wire_len, n,
+                        lens, spos, st, fast);
+        else
+            walk_record(a, wire + start[j], wire + wire_len, pre, r, start[j], end[j], wire_len, n, lens, spos, st,
+                        fast);
     }
 }
 
@@ -928,8 +945,10 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
     __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
-    // bad[0]: some record is not exact (then every tile is copied here)
+    // bad[0]: some record is not exact (then every tile is copied here);
+    // bad[16]: some tile holds chars the walk left (tile_long)
     const bool skip_short = bad && bad[0] == 0;
+    if (skip_short && bad[16] == 0) return;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         // three independent scalar loads issued together (no branch between them)
         const uint32_t needed = tile_long[skip_short ? t : 0] | !skip_short;
@@ -992,8 +1011,10 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t n
 
 // The single-string walk's per-call state in one launch (was three: the
 // status, the exactness flag and a memset of the long-tile marks, ~4-5 us
-// each on the call's critical path).
-__global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* tile_long, uint64_t ntiles) {
+// each on the call's critical path), and the error-path scan's look-back
+// words (k_scan1).
+__global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* tile_long, uint64_t ntiles,
+                              uint64_t* look, uint64_t nlook) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (st) {
             st->flags = 0;
@@ -1001,10 +1022,14 @@ __global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* t
             st->first_bad_record = ~0ull;
         }
         bad[0] = 0;
+        bad[16] = 0;
     }
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < ntiles;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
         tile_long[i] = 0;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nlook;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        look[i] = 0;
 }
 
 // ---- record-tile pack: one pass over the inputs -------------------------------------
@@ -1665,6 +1690,71 @@ __device__ __forceinline__ uint64_t look_back2(uint64_t* look1, uint64_t* look2,
         if (q == 63 && !done) look_store(look2 + blk * stride, kLookIncl | ((pre + total) & kLookVal));
     }
     return pre;
+}
+
+// The gated error-path scan in ONE launch (was reduce + partials + apply,
+// three launches of ~3.7 us each even as no-ops on an exact batch): out[i] =
+// exclusive prefix of f over [0, i), out[n] = total, tile metadata as
+// k_scan_apply's.  Scan block b = ticket order (look[0]), its base by the
+// decoupled look-back over the blocks' totals (look + 1, look2); a bounded
+// grid takes tickets until the blocks run out (a block waits only on lower
+// tickets, taken by running workgroups that wait on nothing later).
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_scan1(F f, uint64_t n, uint64_t* out, uint64_t* tile_first,
+                                                  uint64_t max_tiles, const uint32_t* gate, uint64_t* look,
+                                                  uint64_t* look2, srpc_unpack_status* st) {
+    if (*gate == 0) return;
+    __shared__ uint64_t v[kScanBlock];
+    __shared__ uint64_t s_bx, s_pre;
+    const uint64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    for (;;) {
+        if (threadIdx.x == 0) s_bx = atomicAdd(reinterpret_cast<unsigned long long*>(look), 1ull);
+        __syncthreads();
+        const uint64_t bx = s_bx;
+        if (bx >= nb) break;
+        const uint64_t base = bx * kScanBlock;
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = j * kBlock + threadIdx.x;
+            v[k] = (base + k < n) ? f(base + k) : 0;
+        }
+        __syncthreads();
+        uint64_t loc[kScanItems];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) {
+            loc[j] = sum;
+            sum += v[threadIdx.x * kScanItems + j];
+        }
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(sum, &tot);
+        if (threadIdx.x < 64) {
+            bool stalled = false;
+            const uint64_t pre = look_back2(look + 1, look2, bx, 1, tot, &stalled);
+            if (threadIdx.x == 0) {
+                s_pre = pre;
+                if (stalled && st) report_bad(st, SRPC_STATUS_STALLED, base);
+            }
+        }
+        __syncthreads();
+        const uint64_t pre = s_pre + ex;
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = threadIdx.x * kScanItems + j;
+            const uint64_t start = pre + loc[j], end = start + v[k];
+            for (uint64_t t = (start + kTileBytes - 1) / kTileBytes; t * kTileBytes < end && t < max_tiles; ++t)
+                tile_first[t] = base + k;
+            v[k] = start;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = j * kBlock + threadIdx.x;
+            if (base + k < n) out[base + k] = v[k];
+        }
+        if (bx == nb - 1 && threadIdx.x == 0) out[n] = s_pre + tot;
+        __syncthreads();  // (v and s_bx are rewritten by the next block)
+    }
 }
 
 struct RtuArgs {
@@ -2612,8 +2702,11 @@ int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t 
         for (uint32_t g = 0; g < f; ++g) len_at += p->size[g];
         auto* tile_long = reinterpret_cast<uint32_t*>(base + L.long_off);
         const uint32_t rgrid = static_cast<uint32_t>(std::min<uint64_t>((L.max_tiles + 255) / 256 + 1, 1024));
+        auto* look = reinterpret_cast<uint64_t*>(base + L.look_off);
+        const uint64_t snb = std::max<uint64_t>(1, scan_blocks(n));
+        const uint64_t nlook = 1 + snb + (snb + 63) / 64;  // ticket, per scan block, per 64 blocks
         hipLaunchKernelGGL(k_reset_walk1, dim3(rgrid), dim3(256), 0, s, st_done ? nullptr : st, bad, tile_long,
-                           static_cast<uint64_t>(L.max_tiles));
+                           static_cast<uint64_t>(L.max_tiles), look, nlook);
         st_done = true;
         if (hipGetLastError() != hipSuccess) return SRPC_E_HIP;
         const SingleFast fast{str_offs[f], tiles, L.max_tiles, bad, static_cast<uint8_t*>(cols[f]), tile_long,
@@ -2621,17 +2714,30 @@ int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t 
         // the walk stages its span as in the multi-string path when it fits
         // (0-32 B strings 77 -> 71 us, r01_var_staged_walk_ab.log)
         const uint64_t avg1 = wire_len / n;
-        const uint64_t want1 = avg1 > kWalkStageMax ? ~0ull : stage_bytes_for(avg1);
-        if (want1 <= kWalkStageMax)
-            launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+        // records under kWalkTwoPerLane bytes on average: two per lane (512-record
+        // workgroups; 0-16 B strings' walk 89 -> 76 us, 0-32 B unchanged,
+        // four per lane slower on both: profiles/r06_var_walk_ab.log)
+        const uint32_t kR = avg1 <= kWalkTwoPerLane ? 2 : 1;
+        const uint64_t want1 = avg1 > kWalkStageMax ? ~0ull : stage_bytes_for(avg1, kR);
+        const uint64_t want1s = avg1 > kWalkStageMax ? ~0ull : stage_bytes_for(avg1);
+        if (kR > 1 && want1 <= kWalkStageMax) {
+            const uint64_t g = (n + kBlock * kR - 1) / (kBlock * kR);
+            launch(k_unpack_var_walk<true, 2>, dim3(static_cast<uint32_t>(g)), dim3(kBlock),
                    static_cast<uint32_t>(want1), s, a, wire, wire_len, rec_offs, n, lens, spos, st, fast,
                    static_cast<uint32_t>(want1));
-        else
-            launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+        } else if (want1s <= kWalkStageMax) {
+            launch(k_unpack_var_walk<true, 1>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                   static_cast<uint32_t>(want1s), s, a, wire, wire_len, rec_offs, n, lens, spos, st, fast,
+                   static_cast<uint32_t>(want1s));
+        } else {
+            launch(k_unpack_var_walk<false, 1>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
                    wire_len, rec_offs, n, lens, spos, st, fast, 0u);
-        int rc = launch_scan(SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes},
-                             n, partial, str_offs[f], tiles, L.max_tiles, s, kTileBytes, 1, bad);
-        if (rc) return rc;
+        }
+        if (snb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
+        launch(k_scan1<SingleStrLen>, dim3(static_cast<uint32_t>(std::min<uint64_t>(snb, kGatedGrid))), dim3(kBlock),
+               0, s, SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes}, n,
+               str_offs[f], tiles, static_cast<uint64_t>(L.max_tiles), static_cast<const uint32_t*>(bad), look,
+               look + 1 + snb, st);
         launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f], tiles,
                static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8,
                static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad));
@@ -2644,11 +2750,11 @@ int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t 
         const uint64_t avg = wire_len / n;
         const uint64_t want = avg > kWalkStageMax ? ~0ull : stage_bytes_for(avg);
         if (want <= kWalkStageMax)
-            launch(k_unpack_var_walk<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+            launch(k_unpack_var_walk<true, 1>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
                    static_cast<uint32_t>(want), s, a, wire, wire_len, rec_offs, n, lens, spos, st, SingleFast{},
                    static_cast<uint32_t>(want));
         else
-            launch(k_unpack_var_walk<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
+            launch(k_unpack_var_walk<false, 1>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), 0, s, a, wire,
                    wire_len, rec_offs, n, lens, spos, st, SingleFast{}, 0u);
     }
 #ifndef SRPC_SCAN_PERFIELD
