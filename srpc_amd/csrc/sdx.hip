@@ -103,6 +103,7 @@ constexpr uint32_t kMaxRec = kSB / 8;            // records starting in a block 
 constexpr uint32_t kHugeLog2 = 13;               // strings from 8 KiB: copied by the whole block
 constexpr uint16_t kFar = 0xFFFF;
 constexpr uint32_t kWaveCopyAvg = 128;  // chars per record from which the decode copies a wave per record
+constexpr uint32_t kFarList = 32;       // records of a block whose chars the decode copies from global memory
 constexpr uint32_t kPlausPrefixed = 1, kPlausBare = 2;
 constexpr uint16_t kNoStart = 0xFFFF;
 constexpr uint8_t kNoSpec = 0xFF;
@@ -2433,6 +2434,38 @@ __global__ __launch_bounds__(kBlock) void k_sx_blocks(SxArgs a, const uint8_t* _
 }
 
 // ---- phase 3: the records of every block ----------------------------------------
+// len bytes of the wire at p -> d, by `lanes` lanes (this one `lane`):
+// aligned 16-byte stores built from aligned dword loads (funnel shifts), the
+// unaligned head and tail of d byte by byte (lanes 0 and 1, or lane 0 alone);
+// never a load past the wire's W bytes.
+__device__ __forceinline__ void copy_global(uint8_t* d, const uint8_t* w, uint64_t p, uint64_t len, uint64_t W,
+                                            uint32_t lane, uint32_t lanes) {
+    const uint64_t a0 = min<uint64_t>(len, (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
+    const uint64_t n16 = (len - a0) >> 4, t0 = a0 + 16 * n16;
+    if (lane == 0)
+#pragma nounroll
+        for (uint64_t x = 0; x < a0; ++x) d[x] = w[p + x];
+    if (lane == (lanes > 1 ? 1u : 0u))
+#pragma nounroll
+        for (uint64_t x = t0; x < len; ++x) d[x] = w[p + x];
+    const uintptr_t wend = reinterpret_cast<uintptr_t>(w + W);
+    for (uint64_t c = lane; c < n16; c += lanes) {
+        const uint8_t* px = w + p + a0 + 16 * c;
+        const uintptr_t ax = reinterpret_cast<uintptr_t>(px) & ~uintptr_t{3};
+        uint8_t* dx = d + a0 + 16 * c;
+        if (ax + 20 <= wend) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(ax);
+            const uint32_t s3 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(px) & 3);
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+            *reinterpret_cast<u32x4*>(dx) =
+                u32x4{__builtin_amdgcn_alignbyte(w1, w0, s3), __builtin_amdgcn_alignbyte(w2, w1, s3),
+                      __builtin_amdgcn_alignbyte(w3, w2, s3), __builtin_amdgcn_alignbyte(w4, w3, s3)};
+        } else {
+            for (uint32_t i = 0; i < 16; ++i) dx[i] = px[i];
+        }
+    }
+}
+
 template <int NC>
 struct DecLds {
     alignas(16) uint8_t pre[kMaxPrefix + 16];
@@ -2452,7 +2485,8 @@ struct DecLds {
     alignas(8) uint16_t tbl[kMaxRec + 4];  // the block's records in order: offset from the block
     uint64_t ws[kBlock / 64];
     uint64_t zm[kZW];  // the zero map (zero-heavy blocks only)
-    uint32_t s_nexp;
+    uint32_t far[kFarList];  // lane-per-record copies whose chars run past the stage (a wave each)
+    uint32_t s_nexp, nfar;
 };
 
 template <int NC, bool kDecode>
@@ -2668,7 +2702,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
                     }
                     len = k < nw ? len : 0;
                     if (tid == 0 && R + k <= n) so[R + k] = P + off;
-                    for (uint64_t i = tid; i < len; i += kBlock) chars[P + off + i] = rd.u8(pos + i);
+                    copy_global(chars + P + off, w, pos, len, W, tid, kBlock);
                     off += len;
                 }
                 __syncthreads();
@@ -2685,7 +2719,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
                 L.u.s.loff[k] = static_cast<uint32_t>(run);
                 run += len;
             }
-            if (tid == 0) L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
+            if (tid == 0) {
+                L.u.s.loff[nrec] = static_cast<uint32_t>(ftot);
+                L.nfar = 0;
+            }
             __syncthreads();
             for (uint32_t k = tid; k < nrec && R + k <= n; k += kBlock) so[R + k] = P + L.u.s.loff[k];
             // len chars from stage offset so to d: bytes up to a 4-byte
@@ -2742,13 +2779,17 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
                     if (!len) continue;
                     const uint64_t sp = chars_at(k);
                     uint8_t* d = chars + P + o;
+                    const uint32_t a0 = min<uint32_t>(len, (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
+                    const uint32_t n16 = (len - a0) >> 4, t0 = a0 + 16 * n16;
                     if (!rd.staged(sp, sp + len)) {
-                        for (uint32_t i = lane; i < len; i += 64) d[i] = rd.u8(sp + i);
+                        // chars past the stage (a record that runs past the
+                        // block): the same aligned 16-byte stores, from aligned
+                        // dword loads of global memory (byte copies took 10 of
+                        // the 15 ms of 410 MiB of zero-filled straddlers)
+                        copy_global(d, w, sp, len, W, lane, 64);
                         continue;
                     }
                     const uint32_t so = static_cast<uint32_t>(sp - rd.base);
-                    const uint32_t a0 = min<uint32_t>(len, (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
-                    const uint32_t n16 = (len - a0) >> 4, t0 = a0 + 16 * n16;
                     if (lane < 2) {  // lane 0 the head, lane 1 the tail (byte stores)
                         const uint32_t x0 = lane ? t0 : 0, x1 = lane ? len : a0;
 #pragma nounroll
@@ -2764,17 +2805,28 @@ __global__ __launch_bounds__(kBlock, 8) void k_sx_decode(SxArgs a, const uint8_t
                     }
                 }
             } else {
-                // lane per record
+                // lane per record; chars that run past the stage (a record
+                // straddling the block's end) are listed and copied a wave
+                // per record below -- a lane's byte loop from global memory
+                // took 670K of a zero-filled straddler block's 760K cycles
                 for (uint32_t k = tid; k < nw; k += kBlock) {
                     const uint32_t o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
                     if (!len) continue;
                     const uint64_t sp = chars_at(k);
                     uint8_t* d = chars + P + o;
                     if (!rd.staged(sp, sp + len)) {
-                        for (uint32_t i = 0; i < len; ++i) d[i] = rd.u8(sp + i);
+                        const uint32_t j = atomicAdd(&L.nfar, 1u);
+                        if (j < kFarList) L.far[j] = k;
+                        else copy_global(d, w, sp, len, W, 0, 1);
                         continue;
                     }
                     copy_run(d, static_cast<uint32_t>(sp - rd.base), len);
+                }
+                __syncthreads();
+                const uint32_t nf = min(L.nfar, kFarList);
+                for (uint32_t j = tid >> 6; j < nf; j += kBlock / 64) {
+                    const uint32_t k = L.far[j], o = L.u.s.loff[k], len = L.u.s.loff[k + 1] - o;
+                    copy_global(chars + P + o, w, chars_at(k), len, W, tid & 63, 64);
                 }
             }
             __syncthreads();

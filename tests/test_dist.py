@@ -81,13 +81,21 @@ def test_sharded_pack_gather_equals_single_batch(world, n, use_comm):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, use_comm, q)) for r in range(world)]
+    # daemon ranks, killed if still alive: a rank stuck in the rendezvous
+    # must not keep the test process from exiting
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, use_comm, q), daemon=True) for r in range(world)]
     for p in procs:
         p.start()
-    got, calls, ops = q.get(timeout=180)
-    for p in procs:
-        p.join(timeout=180)
-        assert p.exitcode == 0
+    try:
+        got, calls, ops = q.get(timeout=180)
+        for p in procs:
+            p.join(timeout=180)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
     want = oracle.pack([oracle.INT32] * 4, oracle.splitmix_columns_i32(4, n), n)
     assert got == want
     if use_comm:

@@ -31,6 +31,7 @@ def main():
     import oracle
     import srpc_amd
     from srpc_amd import GpuPacker, Schema
+    from tests.streams import straddler_stream
     from tools.stream_bench import gen_random, gen_zero_heavy
 
     lib = srpc_amd._lib.lib()
@@ -44,7 +45,11 @@ def main():
              ("string_0-16_8M", [S], 1 << 23, lambda k, n, r: gen_random(k, n, r, 16), b""),
              ("string_0-1024_1M", [S], 1 << 20, lambda k, n, r: gen_random(k, n, r, 1024), b""),
              ("zh4_zero_heavy_4M", [I8, S, oracle.INT16, S], 1 << 22, gen_zero_heavy, b""),
-             ("zh4_random_4M", [I8, S, oracle.INT16, S], 1 << 22, lambda k, n, r: gen_random(k, n, r, 24), b"")]
+             ("zh4_random_4M", [I8, S, oracle.INT16, S], 1 << 22, lambda k, n, r: gen_random(k, n, r, 24), b""),
+             ("zh4_straddle_zero_long_1M", [I8, S, oracle.INT16, S], 1 << 20,
+              lambda k, n, r: straddler_stream(n, r, (1, 6000), (65, 6000), "zero"), b""),
+             ("zh4_straddle_heavy_long_1M", [I8, S, oracle.INT16, S], 1 << 20,
+              lambda k, n, r: straddler_stream(n, r, (1100, 6000), (65, 6000), "heavy"), b"")]
     for name, kinds, n, gen, prefix in cases:
         if args.only not in name:
             continue
