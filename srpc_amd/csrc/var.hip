@@ -2296,13 +2296,6 @@ __global__ void k_str_offs_zero(VarArgs a) {  // n == 0: str_offs[f][0] = 0
     if (f < a.nfields && !a.size[f]) const_cast<uint64_t*>(a.soff[f])[0] = 0;
 }
 
-__global__ void k_zero_u64_gated(uint64_t* p, uint64_t count, const uint32_t* gate) {
-    if (*gate == 0) return;
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
-         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-        p[i] = 0;
-}
-
 __global__ void k_zero_u64(uint64_t* p, uint64_t count) {
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
@@ -2671,21 +2664,24 @@ int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t 
         const uint64_t words = 1 + w1 + w2;
         const uint32_t zgrid = static_cast<uint32_t>(std::min<uint64_t>((words + 255) / 256, 1024));
         const uint64_t* no_table = nullptr;
+        // (the optimistic passes below never touch the look-back words: the
+        // status, the flag and the words of the gated look-back pass are
+        // reset in one launch before them, not by a gated launch between)
         if (p->nstrings == 1) {
-            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st_done ? nullptr : st, bad, 1u);
+            hipLaunchKernelGGL(k_reset_walk1, dim3(zgrid), dim3(256), 0, s, st_done ? nullptr : st, bad,
+                               static_cast<uint32_t*>(nullptr), 0ull, look, words);
             st_done = true;
             launch(k_unpack_var_rt<true>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
                    wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad,
                    no_table);
-            launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
         } else if (table) {
             // the tiles' bases from the caller's table; the look-back pass only
             // when a tile's totals disagree with it
-            hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, s, st_done ? nullptr : st, bad, 1u);
+            hipLaunchKernelGGL(k_reset_walk1, dim3(zgrid), dim3(256), 0, s, st_done ? nullptr : st, bad,
+                               static_cast<uint32_t*>(nullptr), 0ull, look, words);
             st_done = true;
             launch(k_unpack_var_rt<false>, dim3(static_cast<uint32_t>(grid)), dim3(kBlock), rlds, s, a, R, wire,
                    wire_len, rec_offs, n, look + 1, look + 1 + w1, reinterpret_cast<uint32_t*>(look), st, bad, table);
-            launch(k_zero_u64_gated, dim3(zgrid), dim3(256), 0, s, look, words, static_cast<const uint32_t*>(bad));
         } else {
             if (!reset_st()) return SRPC_E_HIP;
             launch(k_zero_u64, dim3(zgrid), dim3(256), 0, s, look, words);
