@@ -570,6 +570,43 @@ def test_strings_many_tiles_vs_oracle(schema, maxlen, envelope):
         assert sback[f].tobytes() == back[f].tobytes(), f
 
 
+@pytest.mark.parametrize("envelope", [None, "request"])
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 4099])
+def test_long_records_pack_vs_oracle_and_capacity(n, envelope):
+    """Records of 256 B or more on average (too long for the record tiles'
+    LDS image: the output-chunk walk, k_pack_var) byte for byte against the
+    oracle, and with a wire capacity short of the batch: exactly the bytes
+    before the capacity are written, nothing past it, and BOUNDS is reported
+    at the record that crosses it."""
+    kinds = [oracle.INT16, oracle.STRING, oracle.INT8, oracle.STRING]
+    rng = np.random.default_rng(n + 11)
+    cols, offs = _random_string_batch(kinds, n, rng, 1400)
+    sch = Schema("L", tuple((f"f{i}", k) for i, k in enumerate(kinds)))
+    p = GpuPacker.for_request(sch, "Svc_servicer::m") if envelope else GpuPacker(sch)
+    want = oracle.pack(kinds, cols, n, p.prefix, list(offs))
+    if len(want) // n < 256:  # (a draw of short records: not this path)
+        pytest.skip("average record under 256 B")
+    wire, rec, st = gpu_pack_var(p, kinds, cols, offs, n)
+    assert st == (0, 2**64 - 1) and wire == want
+    # a capacity inside the batch
+    cap = len(want) * 2 // 3 + 5
+    dcols = [dev(c) for c in cols]
+    doffs = [_dev_u64(o) if o is not None else None for o in offs]
+    w = empty(len(want) + 64)
+    recd = empty(8 * (n + 1))
+    sb = p.var_scratch_bytes(n, cap)
+    scratch = empty(sb + 16)
+    stb = status_buf()
+    p.pack_var(dcols, doffs, n, w, cap, recd, scratch, sb, stb)
+    got = host(w, len(want) + 64).tobytes()
+    assert got[:cap] == want[:cap]
+    assert got[cap:] == bytes([0xA5]) * (len(want) + 64 - cap)
+    flags, first = read_status(stb)
+    starts = np.asarray(rec[:n], np.uint64)
+    assert flags & srpc_amd.SRPC_STATUS_BOUNDS
+    assert first == int(np.searchsorted(starts, cap, side="right")) - 1
+
+
 @pytest.mark.parametrize("maxlens", [(0, 700), (3, 0, 900), (700, 2, 40), (0, 0)])
 @pytest.mark.parametrize("n", [1, 257, 6000])
 def test_strings_skewed_fields_vs_oracle(n, maxlens):
