@@ -489,7 +489,7 @@ struct SingleFast {
     uint64_t* soff1;       // str_offs of the string field (n + 1)
     uint64_t* tiles;       // chars tiles' first records
     uint64_t max_tiles;
-    uint32_t* bad;         // [0] some record is not exact, [16] some chars tile is left to the chars kernel
+    uint32_t* bad;         // [0] some record is not exact, [16 k], k = 1 .. kLongFlags - 1: some chars tile is left to the chars kernel
     uint8_t* chars;        // the string field's output chars
     uint32_t* tile_long;   // per chars tile: 1 = it holds chars the walk did not copy
     uint32_t chars_at;     // chars start this many bytes into a record
@@ -717,8 +717,8 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
         const bool exact = flag != SRPC_STATUS_BOUNDS && pos == end && start >= first &&
                            start - first >= r * a.fixed_bytes && o <= wire_len && len <= wire_len - o;
         // a wave whose strings are all short copies them here; otherwise its
-        // strings' chars tiles are left to k_unpack_var_chars (bad[16] says
-        // some tile is, else that launch has nothing to do)
+        // strings' chars tiles are left to k_unpack_str1_tail (a flag below
+        // says some tile is, else that launch has nothing to do)
         const bool all_short = __all(exact && len <= kShortCopy);
         if (exact) {
             for (uint64_t t = (o + kTileBytes - 1) / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
@@ -728,11 +728,16 @@ __device__ __forceinline__ void walk_record(const VarArgs& a, const uint8_t* src
             } else {
                 for (uint64_t t = o / kTileBytes; t * kTileBytes < o + len && t < fast.max_tiles; ++t)
                     fast.tile_long[t] = 1;
-                fast.bad[16] = 1;
             }
         } else {
             atomicOr(fast.bad, 1u);
         }
+        // some chars tile is left to the chars kernel: one store per wave, to
+        // one of kLongFlags flags (a flag per lane of every long wave, all on
+        // one address, cost 0-1024 B strings 108 us)
+        const uint64_t act = __ballot(exact && !all_short);
+        if (act && (threadIdx.x & 63) == static_cast<uint32_t>(__builtin_ctzll(__ballot(1))))
+            fast.bad[16 * (1 + (blockIdx.x + (threadIdx.x >> 6)) % (kLongFlags - 1))] = 1;
     } else if (flag == SRPC_STATUS_BOUNDS) {  // positions are untrustworthy: decode nothing of this record's strings
         for (uint32_t si = 0; si < a.nstrings; ++si) lens[si * n + r] = 0;
     }
@@ -945,10 +950,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_var_chars(const uint8_t* __re
     __shared__ __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
     const uint64_t total = soff[n];
     const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
-    // bad[0]: some record is not exact (then every tile is copied here);
-    // bad[16]: some tile holds chars the walk left (tile_long)
+    // bad[0]: some record is not exact (then every tile is copied here)
     const bool skip_short = bad && bad[0] == 0;
-    if (skip_short && bad[16] == 0) return;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         // three independent scalar loads issued together (no branch between them)
         const uint32_t needed = tile_long[skip_short ? t : 0] | !skip_short;
@@ -1012,7 +1015,7 @@ __global__ void k_reset_status(srpc_unpack_status* st, uint32_t* bad, uint32_t n
 // The single-string walk's per-call state in one launch (was three: the
 // status, the exactness flag and a memset of the long-tile marks, ~4-5 us
 // each on the call's critical path), and the error-path scan's look-back
-// words (k_scan1).
+// words (k_unpack_str1_tail).
 __global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* tile_long, uint64_t ntiles,
                               uint64_t* look, uint64_t nlook) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1022,8 +1025,9 @@ __global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* t
             st->first_bad_record = ~0ull;
         }
         bad[0] = 0;
-        bad[16] = 0;
     }
+    if (blockIdx.x == 0)
+        for (uint32_t i = 1 + threadIdx.x; i < kLongFlags; i += blockDim.x) bad[16 * i] = 0;
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < ntiles;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
         tile_long[i] = 0;
@@ -1753,6 +1757,102 @@ __global__ __launch_bounds__(kBlock) void k_scan1(F f, uint64_t n, uint64_t* out
             if (base + k < n) out[base + k] = v[k];
         }
         if (bx == nb - 1 && threadIdx.x == 0) out[n] = s_pre + tot;
+        __syncthreads();  // (v and s_bx are rewritten by the next block)
+    }
+}
+
+// The single-string walk's tail in ONE gated launch (was the error path's
+// reduce + partials + apply and the chars kernel: four launches of ~3.7 us
+// each, no-ops on an exact batch of short strings):
+// - bad[0] (some record is not exact): str_offs[i] = exclusive prefix of the
+//   decoded lengths (SingleStrLen), str_offs[n] = total, and every record's
+//   chars copied by its lane.  Scan block b = ticket order (look[0]), its
+//   base by the decoupled look-back over the blocks' totals (look + 1,
+//   look2); the grid takes tickets until the blocks run out (a block waits
+//   only on lower tickets, taken by running workgroups that wait on nothing
+//   later);
+// - else one of the long flags bad[16 k] (a wave left long strings): the
+//   chars tiles it marked (tile_long), as k_unpack_var_chars;
+// - else nothing.
+__global__ __launch_bounds__(kBlock) void k_unpack_str1_tail(SingleStrLen f, uint64_t n, uint64_t* soff,
+                                                             uint8_t* __restrict__ chars, uint32_t chars_at,
+                                                             const uint64_t* __restrict__ tiles,
+                                                             const uint32_t* __restrict__ tile_long,
+                                                             const uint32_t* bad, uint64_t* look, uint64_t* look2,
+                                                             srpc_unpack_status* st) {
+    const bool dirty = bad[0] != 0;
+    const bool lng = threadIdx.x >= 1 && threadIdx.x < kLongFlags && bad[16 * threadIdx.x] != 0;
+    if (!__syncthreads_or(dirty || lng)) return;
+    // one LDS region: the chars tiles' windows and slots, or the scan block
+    // (members of one __shared__ object, so every access stays an LDS one)
+    __shared__ union {
+        struct {
+            uint64_t win[kWindow];
+            uint64_t rwin[kWindow];
+            __attribute__((aligned(16))) uint8_t slots[kBlock * 32];
+        } c;
+        uint64_t v[kScanBlock];
+    } U;
+    if (!dirty) {
+        const uint64_t total = soff[n];
+        const uint64_t ntiles = (total + kTileBytes - 1) / kTileBytes;
+        for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            const uint32_t needed = tile_long[t];
+            const uint64_t r0 = tiles[t], r1 = tiles[min(t + 1, ntiles - 1)];
+            asm volatile("" ::"s"(r0), "s"(r1));  // keeps the tile_first loads above the branch
+            if (!needed) continue;
+            chars_tile<false>(f.wire, f.wire_len, soff, nullptr, n, chars, f.rec, chars_at, t, ntiles, total, r0, r1,
+                              U.c.win, U.c.rwin, U.c.slots);
+            __syncthreads();
+        }
+        return;
+    }
+    uint64_t* v = U.v;  // the scan block's values
+    __shared__ uint64_t s_bx, s_pre;
+    const uint64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    for (;;) {
+        if (threadIdx.x == 0) s_bx = atomicAdd(reinterpret_cast<unsigned long long*>(look), 1ull);
+        __syncthreads();
+        const uint64_t bx = s_bx;
+        if (bx >= nb) break;
+        const uint64_t base = bx * kScanBlock;
+#pragma unroll 2
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = j * kBlock + threadIdx.x;
+            v[k] = (base + k < n) ? f(base + k) : 0;
+        }
+        __syncthreads();
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) sum += v[threadIdx.x * kScanItems + j];
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(sum, &tot);
+        if (threadIdx.x < 64) {
+            bool stalled = false;
+            const uint64_t pre = look_back2(look + 1, look2, bx, 1, tot, &stalled);
+            if (threadIdx.x == 0) {
+                s_pre = pre;
+                if (stalled && st) report_bad(st, SRPC_STATUS_STALLED, base);
+            }
+        }
+        __syncthreads();
+        uint64_t run = s_pre + ex;  // this thread's items' offsets, from the lengths still in v
+        const uint8_t* wend = f.wire + f.wire_len;
+#pragma unroll 1
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = threadIdx.x * kScanItems + j;
+            const uint64_t len = v[k];
+            if (len) copy_short(chars + run, f.wire + f.rec[base + k] + chars_at, static_cast<uint32_t>(len), wend);
+            v[k] = run;
+            run += len;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) {
+            const uint32_t k = j * kBlock + threadIdx.x;
+            if (base + k < n) soff[base + k] = v[k];
+        }
+        if (bx == nb - 1 && threadIdx.x == 0) soff[n] = s_pre + tot;
         __syncthreads();  // (v and s_bx are rewritten by the next block)
     }
 }
@@ -2730,13 +2830,24 @@ int srpc_gpu_unpack_var_tiled(const srpc_plan* p, const uint8_t* wire, uint64_t 
                    wire_len, rec_offs, n, lens, spos, st, fast, 0u);
         }
         if (snb > 0x7fffffffull) return SRPC_E_UNSUPPORTED;
-        launch(k_scan1<SingleStrLen>, dim3(static_cast<uint32_t>(std::min<uint64_t>(snb, kGatedGrid))), dim3(kBlock),
-               0, s, SingleStrLen{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes}, n,
-               str_offs[f], tiles, static_cast<uint64_t>(L.max_tiles), static_cast<const uint32_t*>(bad), look,
-               look + 1 + snb, st);
-        launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f], tiles,
-               static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8,
-               static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad));
+        const SingleStrLen lens1{wire, wire_len, rec_offs, p->d_prefix, p->prefix_len, len_at, p->fixed_bytes};
+        if (avg1 <= p->fixed_bytes + kShortCopy) {
+            // short strings: the tail in one gated launch
+            launch(k_unpack_str1_tail, dim3(kVarGrid), dim3(kBlock), 0, s, lens1, n, str_offs[f],
+                   static_cast<uint8_t*>(cols[f]), len_at + 8, static_cast<const uint64_t*>(tiles),
+                   static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad), look, look + 1 + snb,
+                   st);
+        } else {
+            // long strings (the chars kernel copies most tiles): the gated scan,
+            // then the chars kernel on its own (in the tail kernel its tiles ran
+            // 0-1024 B strings 311 -> 420 us, profiles/r06_var_walk_ab.log)
+            launch(k_scan1<SingleStrLen>, dim3(static_cast<uint32_t>(std::min<uint64_t>(snb, kGatedGrid))),
+                   dim3(kBlock), 0, s, lens1, n, str_offs[f], tiles, static_cast<uint64_t>(L.max_tiles),
+                   static_cast<const uint32_t*>(bad), look, look + 1 + snb, st);
+            launch(k_unpack_var_chars, dim3(kVarGrid), dim3(kBlock), 0, s, wire, wire_len, str_offs[f], tiles,
+                   static_cast<const uint64_t*>(nullptr), n, static_cast<uint8_t*>(cols[f]), rec_offs, len_at + 8,
+                   static_cast<const uint32_t*>(tile_long), static_cast<const uint32_t*>(bad));
+        }
         return hipGetLastError() == hipSuccess ? SRPC_OK : SRPC_E_HIP;
     }
     if (!reset_st()) return SRPC_E_HIP;
