@@ -85,7 +85,6 @@ constexpr uint32_t kX = 128;                     // landing slots per block
 #else
 constexpr uint32_t kX = 0;
 #endif
-constexpr uint32_t kXA = kX ? kX : 1;            // (array extents)
 // Exit slots (round 6, the repair pass): the live exits of every chain from
 // every position of the block before (and from longer records of blocks
 // further back), so the cursor's entry into a block is always a slot -- see

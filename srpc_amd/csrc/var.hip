@@ -1060,7 +1060,6 @@ __global__ void k_reset_walk1(srpc_unpack_status* st, uint32_t* bad, uint32_t* t
 // Reference semantics: pack_arg<std::string> (packer.hpp:193-198), records
 // appended back to back (core.hpp:34).
 constexpr uint32_t kRtRegions = 2 * kMaxFields;
-constexpr int kRtBatch = 8;  // staged granule loads in flight per lane
 
 struct RtRegion {
     uint64_t src;  // 16-aligned global address of the region's first granule
@@ -1074,7 +1073,6 @@ struct RtArgs {
     uint32_t img_at;     // image, img_cap bytes
     uint32_t stage_cap, img_cap;
 };
-constexpr uint32_t kRtWin = ((kBlock + 1) * 8 + 16 + 15) & ~15u;  // an offsets window's granules, at most
 constexpr uint64_t kRtImageMin = kBlock * 32;  // the walk's lane slots live in the image
 constexpr uint64_t kRtImageMax = 65536;
 constexpr uint64_t kRtuMinAvg = 40;  // record-tile unpack: smallest average record (bytes)
